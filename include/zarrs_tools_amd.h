@@ -1,0 +1,190 @@
+/*
+ * zarrs_tools_amd.h — the C ABI of the MI355X-native zarrs_filter per-chunk transform path.
+ *
+ * This is the drop-in boundary for the reference's per-chunk filter apply (LDeakin/zarrs_tools
+ * 0.7.2, Rust). A Rust host would bind these symbols through a thin `extern "C"` FFI
+ * (INTEGRATION.md shows the binding); in this repo the host side above the ABI is C++ (the
+ * zarrs_filter / zarrs_ome drivers in zarrs_tools_amd/csrc/host) and Python (ctypes, tests/bench).
+ *
+ * Conventions
+ *  - Plain pointers and sizes only. Array buffers are DEVICE pointers (hipMalloc / torch CUDA
+ *    tensors) unless a function says otherwise. Shapes/strides are int64 element counts, C order
+ *    (last axis fastest), like ndarray's default layout in the reference.
+ *  - Every function returns a zt_status (0 = ok, negative = error); the message of the last error
+ *    on the calling thread is available from zt_last_error().
+ *  - Compute calls are asynchronous on the context's HIP stream; zt_ctx_synchronize() waits.
+ *    Contexts are thread-safe across distinct contexts, not re-entrant on one context.
+ *  - The library never frees caller memory.
+ */
+#ifndef ZARRS_TOOLS_AMD_H
+#define ZARRS_TOOLS_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ZT_ABI_VERSION 1
+#define ZT_MAX_DIMS 8
+
+/* Status codes. Negative values mirror FilterError variants (src/filter/filter_error.rs:10-30). */
+typedef enum zt_status {
+    ZT_OK = 0,
+    ZT_ERR_INVALID_PARAMETERS = -1,   /* FilterError::InvalidParameters */
+    ZT_ERR_UNSUPPORTED_DATA_TYPE = -2,/* FilterError::UnsupportedDataType (filter.rs:93-101) */
+    ZT_ERR_OUT_OF_MEMORY = -3,        /* calculate_chunk_limit "not enough memory" (filter.rs:52-66) */
+    ZT_ERR_DEVICE = -4,               /* HIP runtime error (no reference analogue: CPU-only) */
+    ZT_ERR_STORAGE = -5,              /* FilterError::StorageError */
+    ZT_ERR_ARRAY = -6,                /* FilterError::ArrayError / ArrayCreateError */
+    ZT_ERR_IO = -7,                   /* FilterError::IOError */
+    ZT_ERR_JSON = -8,                 /* FilterError::JSONError */
+    ZT_ERR_INCOMPATIBLE_FILL_VALUE = -9, /* FilterError::IncompatibleFillValue */
+    ZT_ERR_OTHER = -10                /* FilterError::Other */
+} zt_status;
+
+/* Element types accepted by the filters (guided_filter.rs:203-227, downsample.rs:124-148).
+ * Bool is stored as one byte and processed as u8, exactly as the reference's dispatch does
+ * (guided_filter.rs:280, downsample.rs:244). bfloat16/float16 are raw 16-bit storage. */
+typedef enum zt_dtype {
+    ZT_BOOL = 0, ZT_INT8 = 1, ZT_INT16 = 2, ZT_INT32 = 3, ZT_INT64 = 4,
+    ZT_UINT8 = 5, ZT_UINT16 = 6, ZT_UINT32 = 7, ZT_UINT64 = 8,
+    ZT_BFLOAT16 = 9, ZT_FLOAT16 = 10, ZT_FLOAT32 = 11, ZT_FLOAT64 = 12
+} zt_dtype;
+
+typedef struct zt_ctx zt_ctx;
+
+/* ---- library / context ---------------------------------------------------------------------- */
+
+int zt_abi_version(void);
+/* Thread-local message of the last error raised on this thread ("" if none). */
+const char* zt_last_error(void);
+/* Size in bytes of one element of `dtype` (0 for an unknown code). */
+size_t zt_dtype_size(int dtype);
+/* Number of HIP devices visible (0 on a host without GPUs; never an error). */
+int zt_device_count(int* count);
+
+/* One context per (host thread, device): owns a HIP stream, events and reusable scratch. */
+int zt_ctx_create(int device, zt_ctx** out);
+int zt_ctx_destroy(zt_ctx* ctx);
+/* Run subsequent work on an external stream (e.g. torch.cuda.current_stream().cuda_stream).
+ * The handle is used verbatim: NULL is the device's default (null) stream. */
+int zt_ctx_set_stream(zt_ctx* ctx, void* hip_stream);
+/* Return to the context's own (non-blocking) stream, the state after zt_ctx_create. */
+int zt_ctx_use_own_stream(zt_ctx* ctx);
+int zt_ctx_get_stream(zt_ctx* ctx, void** hip_stream);
+int zt_ctx_synchronize(zt_ctx* ctx);
+/* Device time in ms of the most recent filter launch recorded on this context (hipEvents around
+ * the kernel(s) on the context stream). Valid after zt_ctx_synchronize(). */
+int zt_ctx_last_kernel_ms(zt_ctx* ctx, float* ms);
+
+/* ---- operator surface: guided filter -------------------------------------------------------- */
+
+/* GuidedFilter::is_compatible (guided_filter.rs:203-227): ZT_OK or ZT_ERR_UNSUPPORTED_DATA_TYPE. */
+int zt_guided_filter_is_compatible(int dtype_in, int dtype_out);
+/* GuidedFilter::memory_per_chunk (guided_filter.rs:229-238), bytes for one output chunk. */
+int zt_guided_filter_memory_per_chunk(int dtype_in, int dtype_out, const int64_t* chunk_shape,
+                                      int ndim, uint64_t* bytes);
+/* ArraySubsetOverlap::new (array_subset_overlap.rs:11-35) with overlap = 2*radius per axis
+ * (guided_filter.rs:88-93): the halo'd input subset of an output subset, clamped to the array,
+ * and where the output lies inside it. Host-only, no device work. */
+int zt_subset_overlap(const int64_t* array_shape, int ndim, const int64_t* subset_start,
+                      const int64_t* subset_shape, const int64_t* overlap,
+                      int64_t* input_start, int64_t* input_shape, int64_t* dst_in_src_start);
+
+/*
+ * GuidedFilter::apply_ndarray + ArraySubsetOverlap::extract_subset + the TIn->f32 / f32->TOut
+ * `as` casts of apply_chunk (guided_filter.rs:98-103, :117-164).
+ *   in        : device pointer to the (halo'd) input block of `dtype_in`, shape in_shape[ndim],
+ *               element strides in_strides (NULL = C-contiguous). Windows clamp to this block,
+ *               as get_block (guided_filter.rs:166-184) clamps to the SAT's shape.
+ *   out_start : where the output region starts inside the block (dst_in_src); out_shape its shape.
+ *   out       : device pointer, `dtype_out`, shape out_shape, strides out_strides (NULL = C).
+ *   epsilon, radius : GuidedFilterArguments (guided_filter.rs:25-33); radius in [0, 127]
+ *               (the reference's u8 `radius*2` halo overflows above that).
+ * ndim in [1, 8]. 1-3 dims run the fused 2.5-D kernel; 4+ dims run the separable path.
+ */
+int zt_guided_filter_apply_ndarray(zt_ctx* ctx, int dtype_in, const void* in,
+                                   const int64_t* in_shape, const int64_t* in_strides, int ndim,
+                                   const int64_t* out_start, const int64_t* out_shape,
+                                   int dtype_out, void* out, const int64_t* out_strides,
+                                   float epsilon, int radius);
+
+/*
+ * GuidedFilter::apply (guided_filter.rs:240-319) over a device-resident array: every output chunk
+ * of the chunk grid [chunk_grid_start, chunk_grid_start + chunk_grid_count) is filtered with its
+ * 2r halo read from `in` (the whole array, C-contiguous, shape[ndim]) and written into `out`
+ * (same shape, C-contiguous). Pass NULL for the grid range to process every chunk. The chunks are
+ * batched into as few launches as the grid allows (one launch for a box of chunks of a 1-3 D
+ * array); the result equals the reference's chunk-by-chunk result because every window clamps at
+ * the array bounds exactly as the reference's clamped 2r halo makes it.
+ */
+int zt_guided_filter_apply_array(zt_ctx* ctx, int dtype_in, const void* in, int dtype_out,
+                                 void* out, const int64_t* shape, int ndim,
+                                 const int64_t* chunk_shape, float epsilon, int radius,
+                                 const int64_t* chunk_grid_start,
+                                 const int64_t* chunk_grid_count);
+
+/* Multi-GPU z-slab form used by the sharded bench/driver: `in` holds the global rows
+ * [in_z0, in_z0 + in_nz) of an array whose full shape is global_shape (C-contiguous slab); the
+ * output rows [out_z0, out_z0 + out_nz) (global coordinates, a subset of the input rows, chunk
+ * aligned or not) are written into `out` (C-contiguous, out_nz rows). Windows clamp at the global
+ * array bounds, so the result equals the reference's per-chunk result for those rows as long as
+ * the slab carries a 2r halo (or reaches the array edge). 3-D only. */
+int zt_guided_filter_apply_slab(zt_ctx* ctx, int dtype_in, const void* in, int dtype_out,
+                                void* out, const int64_t* global_shape, int64_t in_z0,
+                                int64_t in_nz, int64_t out_z0, int64_t out_nz,
+                                const int64_t* chunk_shape, float epsilon, int radius);
+
+/* ---- operator surface: downsample ----------------------------------------------------------- */
+
+/* Downsample::is_compatible (downsample.rs:124-148); discrete requires integer/bool input
+ * (downsample.rs:244-256). */
+int zt_downsample_is_compatible(int dtype_in, int dtype_out, int discrete);
+/* Downsample::output_shape (downsample.rs:162-168): max(shape / stride, 1). */
+int zt_downsample_output_shape(const int64_t* in_shape, int ndim, const int64_t* stride,
+                               int64_t* out_shape);
+/* Downsample::input_subset (downsample.rs:64-70). */
+int zt_downsample_input_subset(const int64_t* in_shape, int ndim, const int64_t* stride,
+                               const int64_t* out_start, const int64_t* out_shape,
+                               int64_t* in_start, int64_t* in_subset_shape);
+/*
+ * Downsample::apply_ndarray_continuous / apply_ndarray_discrete (downsample.rs:72-120) on a
+ * device block: window = min(stride, extent) per axis; only complete windows produce output
+ * (exact_chunks); out shape = floor(in_shape / window). Continuous: f64 sum in C order / count,
+ * Rust `as` into dtype_out. Discrete (integer/bool input only): the most frequent value, ties
+ * broken by the smallest value (documented deterministic rule; the reference's tie order is
+ * HashMap iteration order).
+ */
+int zt_downsample_apply_ndarray(zt_ctx* ctx, int dtype_in, const void* in,
+                                const int64_t* in_shape, int ndim, const int64_t* stride,
+                                int discrete, int dtype_out, void* out);
+
+/*
+ * zarrs_ome mean pyramid on a device-resident level 0 (zarrs_ome.rs:515-738, levels computed
+ * on-device without a store round trip): level i = downsample(level i-1) for i in 1..=max_levels,
+ * stopping when every axis has factor 1 or output extent 1 (zarrs_ome.rs:731-737).
+ * `level_ptrs[i-1]` receive the levels (device buffers sized by zt_pyramid_level_shapes).
+ * Returns the number of levels written through *levels_written.
+ */
+int zt_pyramid_level_shapes(const int64_t* shape, int ndim, const int64_t* factor, int max_levels,
+                            int64_t* level_shapes /* [max_levels][ndim] */, int* n_levels);
+int zt_pyramid_downsample(zt_ctx* ctx, int dtype, const void* level0, const int64_t* shape,
+                          int ndim, const int64_t* factor, int max_levels, int discrete,
+                          void* const* level_ptrs, int* levels_written);
+
+/* ---- synthetic inputs ------------------------------------------------------ */
+
+/* v = 500*[x >= nx/2] + 100*U, U = (splitmix64(seed ^ global_index) >> 40) * 2^-24, written for
+ * the global rows [z0, z0 + shape[0]) of an array of shape global_shape (C order, f32). */
+int zt_synth_step_noise_f32(zt_ctx* ctx, float* out, const int64_t* shape, int ndim,
+                            const int64_t* global_shape, int64_t z0, uint64_t seed);
+/* u16 = ((splitmix64(seed ^ global_index) >> 40) * 65535) >> 24. */
+int zt_synth_u16(zt_ctx* ctx, uint16_t* out, const int64_t* shape, int ndim,
+                 const int64_t* global_shape, int64_t z0, uint64_t seed);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ZARRS_TOOLS_AMD_H */

@@ -1,0 +1,197 @@
+"""GPU parity: the HIP guided filter (through the C ABI) against the oracle.
+
+Tolerance: float outputs |gpu - oracle| <= 1e-5 * max(1, |oracle|); integer
+outputs equal except where the f32 result sits within that tolerance of a truncation boundary.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from tests.gpu_util import FLOAT_TOL, from_dev, rel_err, to_dev
+
+pytestmark = pytest.mark.gpu
+
+import zarrs_tools_amd as zt  # noqa: E402  (no skip: the HIP library must load)
+
+
+def gpu_apply(v: np.ndarray, din: str, dout: str, chunk, eps, r):
+    import torch
+    x = to_dev(v, din)
+    y = torch.empty(v.shape, dtype=zt.torch_dtype(dout), device="cuda")
+    zt.GuidedFilter(eps, r).apply(zt.DeviceArray(x, chunk, din), zt.DeviceArray(y, chunk, dout))
+    torch.cuda.synchronize()
+    return from_dev(y, dout)
+
+
+def gpu_apply_chunked(v: np.ndarray, din: str, dout: str, chunk, eps, r):
+    """Reference-shaped path: every chunk reads its halo'd block and runs apply_ndarray."""
+    import itertools
+    import torch
+    x = to_dev(v, din)
+    y = torch.empty(v.shape, dtype=zt.torch_dtype(dout), device="cuda")
+    a_in, a_out = zt.DeviceArray(x, chunk, din), zt.DeviceArray(y, chunk, dout)
+    g = zt.GuidedFilter(eps, r)
+    for idx in itertools.product(*[range(n) for n in a_out.chunk_grid_shape()]):
+        g.apply_chunk(a_in, a_out, idx)
+    torch.cuda.synchronize()
+    return from_dev(y, dout)
+
+
+def check_against(out, ref_f32, dout):
+    if dout in ("float32", "float64"):
+        assert rel_err(out, ref_f32) <= FLOAT_TOL
+    elif dout in ("float16", "bfloat16"):
+        ref = O.cast_from_f32(ref_f32, dout)
+        o32 = O.cast_to_f32(out, dout).astype(np.float64)
+        r32 = O.cast_to_f32(ref, dout).astype(np.float64)
+        ulp = 2.0 ** -10 if dout == "float16" else 2.0 ** -7
+        assert np.all(np.abs(o32 - r32) <= ulp * np.maximum(1.0, np.abs(r32)) + 1e-12)
+    else:
+        ref = O.cast_from_f32(ref_f32, dout)
+        diff = out.astype(np.float64) != ref.astype(np.float64)
+        if diff.any():
+            # only where the f32 value is within tolerance of an integer boundary
+            near = np.abs(ref_f32 - np.round(ref_f32)) <= FLOAT_TOL * np.maximum(1, np.abs(ref_f32))
+            assert np.all(near[diff]), (np.argwhere(diff)[:5], ref_f32[diff][:5])
+            assert np.all(np.abs(out.astype(np.float64) - ref.astype(np.float64))[diff] <= 1)
+
+
+def test_reference_kat_through_c_abi():
+    # guided_filter.rs:330-374: 4x4 f32, 2x2 chunks, eps 1, r 2
+    v = np.array([[i + j for j in range(4)] for i in range(4)], dtype=np.float32)
+    kat = np.array([[1.659829, 2.1910257, 2.5641026, 3.0],
+                    [2.1910257, 2.614423, 3.0, 3.4358974],
+                    [2.5641026, 3.0, 3.385577, 3.8089743],
+                    [3.0, 3.4358974, 3.8089743, 4.340171]], dtype=np.float32)
+    out = gpu_apply(v, "float32", "float32", (2, 2), 1.0, 2)
+    assert rel_err(out, kat) <= FLOAT_TOL
+    out2 = gpu_apply_chunked(v, "float32", "float32", (2, 2), 1.0, 2)
+    assert rel_err(out2, kat) <= FLOAT_TOL
+    print("KAT max abs diff", np.abs(out - kat).max(), "bit-exact", np.array_equal(out, kat))
+
+
+def _golden(golden_dir, name, kind):
+    return np.load(os.path.join(golden_dir, f"{name}_{kind}.npy"))
+
+
+def test_golden_whole_array(golden_cases, golden_dir):
+    for c in golden_cases["guided_filter"]:
+        vin = _golden(golden_dir, c["name"], "in")
+        ref = _golden(golden_dir, c["name"], "out_f32")
+        out = gpu_apply(vin, c["dtype_in"], c["dtype_out"], c["chunk_shape"], c["epsilon"],
+                        c["radius"])
+        check_against(out, ref, c["dtype_out"])
+
+
+def test_golden_per_chunk(golden_cases, golden_dir):
+    for c in golden_cases["guided_filter"]:
+        vin = _golden(golden_dir, c["name"], "in")
+        ref = _golden(golden_dir, c["name"], "out_f32")
+        out = gpu_apply_chunked(vin, c["dtype_in"], c["dtype_out"], c["chunk_shape"],
+                                c["epsilon"], c["radius"])
+        check_against(out, ref, c["dtype_out"])
+
+
+@pytest.mark.parametrize("r", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 12])
+def test_radii_3d(r):
+    rng = np.random.default_rng(r)
+    shape = (int(rng.integers(9, 30)), int(rng.integers(9, 70)), int(rng.integers(9, 90)))
+    chunk = tuple(int(rng.integers(4, 20)) for _ in range(3))
+    v = (rng.random(shape, dtype=np.float32) * 300).astype(np.float32)
+    eps = float(rng.choice([0.5, 50.0, 2500.0]))
+    ref = O.guided_filter_apply(v, chunk, eps, r, nthreads=8)
+    out = gpu_apply(v, "float32", "float32", chunk, eps, r)
+    assert rel_err(out, ref) <= FLOAT_TOL, (shape, chunk, eps)
+
+
+def test_radius_zero_is_identity():
+    v = O.synth_step_noise_f32((7, 9, 70))
+    out = gpu_apply(v, "float32", "float32", (4, 4, 32), 2500.0, 0)
+    assert np.array_equal(out, v)
+
+
+@pytest.mark.parametrize("din", list(O.DTYPES))
+def test_all_input_types(din):
+    rng = np.random.default_rng(7)
+    v32 = (rng.random((6, 13, 70), dtype=np.float32) * 200 - (50 if din.startswith("int") else 0))
+    v = O.cast_from_f32(v32, din)
+    ref = O.guided_filter_apply(O.cast_to_f32(v, din), (4, 8, 32), 100.0, 2, nthreads=8)
+    out = gpu_apply(v, din, "float32", (4, 8, 32), 100.0, 2)
+    assert rel_err(out, ref) <= FLOAT_TOL
+
+
+@pytest.mark.parametrize("dout", list(O.DTYPES))
+def test_all_output_types(dout):
+    v = O.synth_step_noise_f32((6, 13, 70)) * np.float32(0.4)
+    ref = O.guided_filter_apply(v, (4, 8, 32), 100.0, 2, nthreads=8)
+    out = gpu_apply(v, "float32", dout, (4, 8, 32), 100.0, 2)
+    check_against(out, ref, dout)
+
+
+def test_degenerate_shapes():
+    for shape in [(0, 5, 5), (1, 1, 1), (1, 1, 300), (3, 1, 1), (1, 65, 1)]:
+        v = O.synth_step_noise_f32(shape) if 0 not in shape else np.zeros(shape, np.float32)
+        ref = O.guided_filter_apply(v, (2, 2, 64), 2500.0, 2) if v.size else v
+        out = gpu_apply(v, "float32", "float32", (2, 2, 64), 2500.0, 2)
+        assert out.shape == v.shape
+        if v.size:
+            assert rel_err(out, ref) <= FLOAT_TOL, shape
+
+
+def test_subset_of_chunk_grid_only_touches_those_chunks():
+    import torch
+    v = O.synth_step_noise_f32((16, 16, 64))
+    ref = O.guided_filter_apply(v, (8, 8, 32), 2500.0, 2)
+    x = to_dev(v, "float32")
+    y = torch.full(v.shape, -1.0, device="cuda")
+    zt.GuidedFilter(2500.0, 2).apply(zt.DeviceArray(x, (8, 8, 32)), zt.DeviceArray(y, (8, 8, 32)),
+                                     chunk_grid_start=(1, 0, 1), chunk_grid_count=(1, 2, 1))
+    out = from_dev(y, "float32")
+    assert rel_err(out[8:, :, 32:], ref[8:, :, 32:]) <= FLOAT_TOL
+    assert np.all(out[:8] == -1) and np.all(out[:, :, :32] == -1)
+
+
+def test_slab_form_equals_whole_array():
+    import torch
+    shape, chunk, r = (48, 40, 96), (16, 16, 32), 4
+    v = O.synth_step_noise_f32(shape)
+    whole = gpu_apply(v, "float32", "float32", chunk, 2500.0, r)
+    x = to_dev(v, "float32")
+    res = np.empty_like(v)
+    for rank in range(3):
+        a = zt.slab_assignment(rank, 3, shape[0], chunk[0], 2 * r)
+        y = torch.empty((a.out_nz,) + shape[1:], device="cuda")
+        slab = x[a.in_z0:a.in_z0 + a.in_nz].contiguous()
+        zt._abi.check(zt._abi.lib().zt_guided_filter_apply_slab(
+            zt.default_context().handle, 11, zt.filter._ptr(slab), 11, zt.filter._ptr(y),
+            zt._abi.i64_array(shape), a.in_z0, a.in_nz, a.out_z0, a.out_nz,
+            zt._abi.i64_array(chunk), 2500.0, r))
+        torch.cuda.synchronize()
+        res[a.out_z0:a.out_z0 + a.out_nz] = from_dev(y, "float32")
+    assert np.array_equal(res, whole)
+
+
+def test_synthetic_generator_matches_oracle():
+    import torch
+    shape = (5, 33, 70)
+    d = zt.synth_step_noise_f32(shape, global_shape=(9, 33, 70), z0=3)
+    torch.cuda.synchronize()
+    assert np.array_equal(from_dev(d, "float32"),
+                          O.synth_step_noise_f32(shape, global_shape=(9, 33, 70), z0=3))
+    u = zt.synth_u16((4, 5, 6), z0=2, global_shape=(8, 5, 6))
+    torch.cuda.synchronize()
+    assert np.array_equal(from_dev(u, "uint16"), O.synth_u16((4, 5, 6), z0=2,
+                                                             global_shape=(8, 5, 6)))
+
+
+def test_256_cube_r4_vs_oracle():
+    shape, chunk = (256, 256, 256), (128, 128, 128)
+    v = O.synth_step_noise_f32(shape)
+    ref = O.guided_filter_apply(v, chunk, 2500.0, 4, nthreads=16)
+    out = gpu_apply(v, "float32", "float32", chunk, 2500.0, 4)
+    err = rel_err(out, ref)
+    exact = float(np.mean(out == ref))
+    print(f"256^3 r=4: max rel err {err:.3e}, bit-exact fraction {exact:.4f}")
+    assert err <= FLOAT_TOL

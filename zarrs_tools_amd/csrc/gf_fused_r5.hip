@@ -1,0 +1,6 @@
+// gf_fused_r5.hip — fused guided-filter instantiations for radius 5.
+#include "gf_fused.hpp"
+
+namespace zt {
+ZT_FUSED_PAIRS(5, 32, 1024)
+}  // namespace zt

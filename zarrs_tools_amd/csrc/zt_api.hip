@@ -1,0 +1,681 @@
+// zt_api.hip — the C ABI (include/zarrs_tools_amd.h): validation, geometry and launches.
+//
+// Host-side restatement of the reference's per-chunk orchestration around the kernels:
+//   chunk_subset_bounded + ArraySubsetOverlap::new/extract_subset (guided_filter.rs:87-103,
+//   array_subset_overlap.rs:11-51), Downsample::input_subset/output_shape (downsample.rs:64-70,
+//   :162-168), is_compatible/memory_per_chunk (guided_filter.rs:203-238, downsample.rs:124-160),
+//   and the zarrs_ome level loop's shapes and stop rule (zarrs_ome.rs:515-560, :731-737).
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/zarrs_tools_amd.h"
+#include "zt_device.hpp"
+#include "zt_kernels.hpp"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+    return fail(ZT_ERR_DEVICE, "%s: %s", what, hipGetErrorString(e));
+}
+
+#define ZT_HIP(call)                                                                             \
+    do {                                                                                         \
+        hipError_t _e = (call);                                                                  \
+        if (_e != hipSuccess) return hip_fail(_e, #call);                                        \
+    } while (0)
+
+bool valid_dtype(int d) { return d >= ZT_BOOL && d <= ZT_FLOAT64; }
+
+const char* dtype_name(int d) {
+    static const char* names[] = {"bool",   "int8",   "int16",    "int32",   "int64",
+                                  "uint8",  "uint16", "uint32",   "uint64",  "bfloat16",
+                                  "float16", "float32", "float64"};
+    return valid_dtype(d) ? names[d] : "unknown";
+}
+
+}  // namespace
+
+struct zt_ctx {
+    int device = 0;
+    hipStream_t own = nullptr;
+    hipStream_t cur = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    bool timed = false;
+    void* scratch = nullptr;
+    size_t scratch_bytes = 0;
+
+    int ensure_scratch(size_t bytes) {
+        if (bytes <= scratch_bytes) return ZT_OK;
+        if (scratch) {
+            (void)hipStreamSynchronize(cur);
+            (void)hipFree(scratch);
+            scratch = nullptr;
+            scratch_bytes = 0;
+        }
+        hipError_t e = hipMalloc(&scratch, bytes);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            return fail(ZT_ERR_OUT_OF_MEMORY, "device scratch of %zu bytes: %s", bytes,
+                        hipGetErrorString(e));
+        }
+        scratch_bytes = bytes;
+        return ZT_OK;
+    }
+};
+
+namespace {
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int now = -1;
+        if (prev >= 0 && hipGetDevice(&now) == hipSuccess && now != prev) (void)hipSetDevice(prev);
+    }
+};
+
+int check_ctx(zt_ctx* ctx) {
+    if (!ctx) return fail(ZT_ERR_INVALID_PARAMETERS, "null context");
+    return ZT_OK;
+}
+
+int check_shape(const int64_t* shape, int ndim, const char* what) {
+    if (ndim < 1 || ndim > ZT_MAX_DIMS)
+        return fail(ZT_ERR_INVALID_PARAMETERS, "%s: ndim %d not in [1, %d]", what, ndim,
+                    ZT_MAX_DIMS);
+    if (!shape) return fail(ZT_ERR_INVALID_PARAMETERS, "%s: null shape", what);
+    for (int d = 0; d < ndim; ++d)
+        if (shape[d] < 0) return fail(ZT_ERR_INVALID_PARAMETERS, "%s: negative extent", what);
+    return ZT_OK;
+}
+
+int64_t numel(const int64_t* s, int n) {
+    int64_t r = 1;
+    for (int i = 0; i < n; ++i) r *= s[i];
+    return r;
+}
+
+void c_strides(const int64_t* shape, int ndim, int64_t* strides) {
+    int64_t s = 1;
+    for (int d = ndim - 1; d >= 0; --d) {
+        strides[d] = s;
+        s *= shape[d];
+    }
+}
+
+// Choose the z-march length for a fused launch: whole chunk depths when there is enough
+// parallelism, shorter segments for a single small block.
+int choose_zseg(int onz, int tiles, int radius, int chunk_depth) {
+    const int target_wg = 1024;
+    int zseg = chunk_depth > 0 ? std::min(chunk_depth, onz) : onz;
+    if (zseg <= 0) zseg = 1;
+    int64_t wg = (int64_t)tiles * ((onz + zseg - 1) / zseg);
+    if (wg < target_wg && chunk_depth <= 0) {
+        int nseg = (target_wg + tiles - 1) / std::max(tiles, 1);
+        int minseg = std::max(8, 4 * radius);
+        zseg = std::max(minseg, (onz + nseg - 1) / nseg);
+        zseg = std::min(zseg, onz);
+    }
+    return zseg;
+}
+
+int radius_ok(int radius) {
+    if (radius < 0 || radius > zt::kMaxRadius)
+        return fail(ZT_ERR_INVALID_PARAMETERS,
+                    "radius %d not in [0, %d] (the reference's u8 halo radius*2 overflows)", radius,
+                    zt::kMaxRadius);
+    return ZT_OK;
+}
+
+int dtypes_ok(int dtype_in, int dtype_out) {
+    if (!valid_dtype(dtype_in))
+        return fail(ZT_ERR_UNSUPPORTED_DATA_TYPE, "Unsupported data type code %d", dtype_in);
+    if (!valid_dtype(dtype_out))
+        return fail(ZT_ERR_UNSUPPORTED_DATA_TYPE, "Unsupported data type code %d", dtype_out);
+    return ZT_OK;
+}
+
+// Fused launch on a 3-D view (pad 1-2 D arrays with leading unit axes).
+int run_fused3(zt_ctx* ctx, int dtype_in, const void* in, const int64_t dom[3], int64_t in_z0,
+               int64_t in_rows, int64_t in_sz, int64_t in_sy, const int64_t ostart[3],
+               const int64_t oshape[3], int dtype_out, void* out, int64_t out_sz, int64_t out_sy,
+               float eps, int radius, int chunk_depth) {
+    for (int d = 0; d < 3; ++d)
+        if (dom[d] > INT32_MAX || oshape[d] > INT32_MAX)
+            return fail(ZT_ERR_INVALID_PARAMETERS, "extent exceeds 2^31-1");
+    zt::GFParams p{};
+    p.in = in;
+    p.out = out;
+    p.in_sz = in_sz;
+    p.in_sy = in_sy;
+    p.out_sz = out_sz;
+    p.out_sy = out_sy;
+    p.in_z0 = (int)in_z0;
+    p.nz = (int)dom[0];
+    p.ny = (int)dom[1];
+    p.nx = (int)dom[2];
+    p.oz0 = (int)ostart[0];
+    p.oy0 = (int)ostart[1];
+    p.ox0 = (int)ostart[2];
+    p.onz = (int)oshape[0];
+    p.ony = (int)oshape[1];
+    p.onx = (int)oshape[2];
+    p.eps = eps;
+    if (p.onz == 0 || p.ony == 0 || p.onx == 0) return ZT_OK;
+    // Pairs without a direct instantiation: stage the input rows and/or the output region
+    // through contiguous f32 scratch (cast kernels with the same Rust `as` semantics).
+    const bool stage_in = !zt::fused_direct_pair(dtype_in, zt::kF32);
+    const bool stage_out = !zt::fused_direct_pair(zt::kF32, dtype_out);
+    const int64_t in_elems = stage_in ? in_rows * dom[1] * dom[2] : 0;
+    const int64_t out_elems = stage_out ? oshape[0] * oshape[1] * oshape[2] : 0;
+    if (stage_in || stage_out) {
+        int rc = ctx->ensure_scratch(sizeof(float) * (size_t)(in_elems + out_elems));
+        if (rc) return rc;
+    }
+    float* sin = static_cast<float*>(ctx->scratch);
+    float* sout = sin + in_elems;
+    if (stage_in) {
+        hipError_t e = zt::launch_cast_to_f32_3d(in, dtype_in, in_sz, in_sy, sin, in_rows, dom[1],
+                                                 dom[2], ctx->cur);
+        if (e != hipSuccess) return hip_fail(e, "input staging cast");
+        p.in = sin;
+        p.in_sz = dom[1] * dom[2];
+        p.in_sy = dom[2];
+        dtype_in = zt::kF32;
+    }
+    if (stage_out) {
+        p.out = sout;
+        p.out_sz = oshape[1] * oshape[2];
+        p.out_sy = oshape[2];
+    }
+    const int ty = zt::fused_tile_y(radius);
+    int tiles = (int)(((p.onx + 63) / 64) * ((p.ony + ty - 1) / ty));
+    p.zseg = choose_zseg(p.onz, tiles, radius, chunk_depth);
+    if (ctx->timed) ZT_HIP(hipEventRecord(ctx->ev0, ctx->cur));
+    hipError_t e = zt::launch_guided_fused(p, dtype_in, stage_out ? (int)zt::kF32 : dtype_out,
+                                           radius, ctx->cur);
+    if (e != hipSuccess) return hip_fail(e, "guided filter fused kernel launch");
+    if (ctx->timed) ZT_HIP(hipEventRecord(ctx->ev1, ctx->cur));
+    if (stage_out) {
+        e = zt::launch_cast_from_f32_3d(sout, dtype_out, out, out_sz, out_sy, oshape[0],
+                                        oshape[1], oshape[2], ctx->cur);
+        if (e != hipSuccess) return hip_fail(e, "output staging cast");
+    }
+    return ZT_OK;
+}
+
+int run_separable(zt_ctx* ctx, int dtype_in, const void* in, const int64_t* shape,
+                  const int64_t* in_strides, int ndim, const int64_t* out_start,
+                  const int64_t* out_shape, int dtype_out, void* out, const int64_t* out_strides,
+                  float eps, int radius) {
+    zt::NdGeom g{};
+    g.ndim = ndim;
+    g.numel = numel(shape, ndim);
+    g.out_numel = numel(out_shape, ndim);
+    for (int d = 0; d < ndim; ++d) {
+        g.shape[d] = shape[d];
+        g.in_strides[d] = in_strides[d];
+        g.out_start[d] = out_start[d];
+        g.out_shape[d] = out_shape[d];
+        g.out_strides[d] = out_strides[d];
+    }
+    if (g.numel == 0 || g.out_numel == 0) return ZT_OK;
+    int rc = ctx->ensure_scratch(sizeof(float) * 5 * (size_t)g.numel);
+    if (rc) return rc;
+    if (ctx->timed) ZT_HIP(hipEventRecord(ctx->ev0, ctx->cur));
+    hipError_t e = zt::launch_guided_separable(in, dtype_in, out, dtype_out, g, radius, eps,
+                                               static_cast<float*>(ctx->scratch), ctx->cur);
+    if (e != hipSuccess) return hip_fail(e, "guided filter separable launch");
+    if (ctx->timed) ZT_HIP(hipEventRecord(ctx->ev1, ctx->cur));
+    return ZT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int zt_abi_version(void) { return ZT_ABI_VERSION; }
+
+const char* zt_last_error(void) { return g_last_error.c_str(); }
+
+size_t zt_dtype_size(int dtype) { return zt::dtype_size(dtype); }
+
+int zt_device_count(int* count) {
+    if (!count) return fail(ZT_ERR_INVALID_PARAMETERS, "null count");
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) {
+        (void)hipGetLastError();
+        n = 0;
+    }
+    *count = n;
+    return ZT_OK;
+}
+
+int zt_ctx_create(int device, zt_ctx** out) {
+    if (!out) return fail(ZT_ERR_INVALID_PARAMETERS, "null output pointer");
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
+        (void)hipGetLastError();
+        return fail(ZT_ERR_DEVICE, "no HIP device available");
+    }
+    if (device < 0 || device >= n)
+        return fail(ZT_ERR_INVALID_PARAMETERS, "device %d not in [0, %d)", device, n);
+    ZT_HIP(hipSetDevice(device));
+    zt_ctx* c = new zt_ctx();
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+        delete c;
+        return fail(ZT_ERR_DEVICE, "stream/event creation failed");
+    }
+    c->cur = c->own;
+    c->timed = true;
+    *out = c;
+    return ZT_OK;
+}
+
+int zt_ctx_destroy(zt_ctx* ctx) {
+    if (!ctx) return ZT_OK;
+    DeviceGuard g(ctx->device);
+    (void)hipStreamSynchronize(ctx->cur);
+    if (ctx->scratch) (void)hipFree(ctx->scratch);
+    if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
+    if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+    if (ctx->own) (void)hipStreamDestroy(ctx->own);
+    delete ctx;
+    return ZT_OK;
+}
+
+int zt_ctx_set_stream(zt_ctx* ctx, void* hip_stream) {
+    if (int rc = check_ctx(ctx)) return rc;
+    // Used verbatim: NULL is the device's default (null) stream, which is what
+    // torch.cuda.current_stream().cuda_stream returns for torch's default stream.
+    ctx->cur = static_cast<hipStream_t>(hip_stream);
+    return ZT_OK;
+}
+
+int zt_ctx_use_own_stream(zt_ctx* ctx) {
+    if (int rc = check_ctx(ctx)) return rc;
+    ctx->cur = ctx->own;
+    return ZT_OK;
+}
+
+int zt_ctx_get_stream(zt_ctx* ctx, void** hip_stream) {
+    if (int rc = check_ctx(ctx)) return rc;
+    if (!hip_stream) return fail(ZT_ERR_INVALID_PARAMETERS, "null output pointer");
+    *hip_stream = ctx->cur;
+    return ZT_OK;
+}
+
+int zt_ctx_synchronize(zt_ctx* ctx) {
+    if (int rc = check_ctx(ctx)) return rc;
+    DeviceGuard g(ctx->device);
+    ZT_HIP(hipStreamSynchronize(ctx->cur));
+    return ZT_OK;
+}
+
+int zt_ctx_last_kernel_ms(zt_ctx* ctx, float* ms) {
+    if (int rc = check_ctx(ctx)) return rc;
+    if (!ms) return fail(ZT_ERR_INVALID_PARAMETERS, "null output pointer");
+    DeviceGuard g(ctx->device);
+    ZT_HIP(hipEventElapsedTime(ms, ctx->ev0, ctx->ev1));
+    return ZT_OK;
+}
+
+// ---- guided filter ---------------------------------------------------------------------------
+
+int zt_guided_filter_is_compatible(int dtype_in, int dtype_out) {
+    // guided_filter.rs:208-224: every listed type is accepted for input and output.
+    return dtypes_ok(dtype_in, dtype_out);
+}
+
+int zt_guided_filter_memory_per_chunk(int dtype_in, int dtype_out, const int64_t* chunk_shape,
+                                      int ndim, uint64_t* bytes) {
+    if (int rc = dtypes_ok(dtype_in, dtype_out)) return rc;
+    if (int rc = check_shape(chunk_shape, ndim, "chunk_shape")) return rc;
+    if (!bytes) return fail(ZT_ERR_INVALID_PARAMETERS, "null output pointer");
+    // guided_filter.rs:234-237 (element sizes + num_elements * (f64 + 2 f32))
+    uint64_t n = (uint64_t)numel(chunk_shape, ndim);
+    *bytes = zt::dtype_size(dtype_in) + zt::dtype_size(dtype_out) + n * (8 + 4 * 2);
+    return ZT_OK;
+}
+
+int zt_subset_overlap(const int64_t* array_shape, int ndim, const int64_t* subset_start,
+                      const int64_t* subset_shape, const int64_t* overlap, int64_t* input_start,
+                      int64_t* input_shape, int64_t* dst_in_src_start) {
+    if (int rc = check_shape(array_shape, ndim, "array_shape")) return rc;
+    if (!subset_start || !subset_shape || !overlap || !input_start || !input_shape ||
+        !dst_in_src_start)
+        return fail(ZT_ERR_INVALID_PARAMETERS, "null pointer argument");
+    for (int d = 0; d < ndim; ++d) {
+        if (overlap[d] < 0 || subset_start[d] < 0 || subset_shape[d] < 0 ||
+            subset_start[d] + subset_shape[d] > array_shape[d])
+            return fail(ZT_ERR_INVALID_PARAMETERS, "subset outside the array on axis %d", d);
+        // array_subset_overlap.rs:12-29
+        int64_t s = subset_start[d] > overlap[d] ? subset_start[d] - overlap[d] : 0;
+        int64_t e = std::min(subset_start[d] + subset_shape[d] + overlap[d], array_shape[d]);
+        input_start[d] = s;
+        input_shape[d] = e - s;
+        dst_in_src_start[d] = subset_start[d] - s;
+    }
+    return ZT_OK;
+}
+
+int zt_guided_filter_apply_ndarray(zt_ctx* ctx, int dtype_in, const void* in,
+                                   const int64_t* in_shape, const int64_t* in_strides, int ndim,
+                                   const int64_t* out_start, const int64_t* out_shape,
+                                   int dtype_out, void* out, const int64_t* out_strides,
+                                   float epsilon, int radius) {
+    if (int rc = check_ctx(ctx)) return rc;
+    if (int rc = dtypes_ok(dtype_in, dtype_out)) return rc;
+    if (int rc = radius_ok(radius)) return rc;
+    if (int rc = check_shape(in_shape, ndim, "in_shape")) return rc;
+    if (!out_start || !out_shape) return fail(ZT_ERR_INVALID_PARAMETERS, "null output region");
+    for (int d = 0; d < ndim; ++d)
+        if (out_start[d] < 0 || out_shape[d] < 0 || out_start[d] + out_shape[d] > in_shape[d])
+            return fail(ZT_ERR_INVALID_PARAMETERS, "output region outside the block on axis %d",
+                        d);
+    if (numel(out_shape, ndim) == 0) return ZT_OK;
+    if (!in || !out) return fail(ZT_ERR_INVALID_PARAMETERS, "null data pointer");
+    int64_t is[ZT_MAX_DIMS], os[ZT_MAX_DIMS];
+    if (in_strides) std::copy(in_strides, in_strides + ndim, is);
+    else c_strides(in_shape, ndim, is);
+    if (out_strides) std::copy(out_strides, out_strides + ndim, os);
+    else c_strides(out_shape, ndim, os);
+    DeviceGuard g(ctx->device);
+    if (ndim <= 3 && zt::fused_supports_radius(radius) && is[ndim - 1] == 1 &&
+        os[ndim - 1] == 1) {
+        int64_t dom[3] = {1, 1, 1}, ost[3] = {0, 0, 0}, osh[3] = {1, 1, 1};
+        int64_t isz = 0, isy = 0, osz = 0, osy = 0;
+        for (int d = 0; d < ndim; ++d) {
+            dom[3 - ndim + d] = in_shape[d];
+            ost[3 - ndim + d] = out_start[d];
+            osh[3 - ndim + d] = out_shape[d];
+        }
+        if (ndim == 3) { isz = is[0]; isy = is[1]; osz = os[0]; osy = os[1]; }
+        if (ndim == 2) { isy = is[0]; osy = os[0]; }
+        return run_fused3(ctx, dtype_in, in, dom, 0, dom[0], isz, isy, ost, osh, dtype_out, out,
+                          osz, osy, epsilon, radius, 0);
+    }
+    return run_separable(ctx, dtype_in, in, in_shape, is, ndim, out_start, out_shape, dtype_out,
+                         out, os, epsilon, radius);
+}
+
+int zt_guided_filter_apply_array(zt_ctx* ctx, int dtype_in, const void* in, int dtype_out,
+                                 void* out, const int64_t* shape, int ndim,
+                                 const int64_t* chunk_shape, float epsilon, int radius,
+                                 const int64_t* chunk_grid_start,
+                                 const int64_t* chunk_grid_count) {
+    if (int rc = check_ctx(ctx)) return rc;
+    if (int rc = dtypes_ok(dtype_in, dtype_out)) return rc;
+    if (int rc = radius_ok(radius)) return rc;
+    if (int rc = check_shape(shape, ndim, "shape")) return rc;
+    if (!chunk_shape) return fail(ZT_ERR_INVALID_PARAMETERS, "null chunk_shape");
+    int64_t grid[ZT_MAX_DIMS], g0[ZT_MAX_DIMS], gn[ZT_MAX_DIMS];
+    for (int d = 0; d < ndim; ++d) {
+        if (chunk_shape[d] <= 0)
+            return fail(ZT_ERR_INVALID_PARAMETERS, "chunk extent must be positive");
+        grid[d] = (shape[d] + chunk_shape[d] - 1) / chunk_shape[d];
+        g0[d] = chunk_grid_start ? chunk_grid_start[d] : 0;
+        gn[d] = chunk_grid_count ? chunk_grid_count[d] : grid[d];
+        if (g0[d] < 0 || gn[d] < 0 || g0[d] + gn[d] > grid[d])
+            return fail(ZT_ERR_INVALID_PARAMETERS, "chunk grid range outside the grid on axis %d",
+                        d);
+    }
+    if (numel(gn, ndim) == 0 || numel(shape, ndim) == 0) return ZT_OK;
+    if (!in || !out) return fail(ZT_ERR_INVALID_PARAMETERS, "null data pointer");
+    // Output region = the box of chunks (chunk_subset_bounded per chunk, guided_filter.rs:87).
+    int64_t ostart[ZT_MAX_DIMS], oshape[ZT_MAX_DIMS], strides[ZT_MAX_DIMS];
+    for (int d = 0; d < ndim; ++d) {
+        ostart[d] = g0[d] * chunk_shape[d];
+        oshape[d] = std::min((g0[d] + gn[d]) * chunk_shape[d], shape[d]) - ostart[d];
+    }
+    c_strides(shape, ndim, strides);
+    DeviceGuard g(ctx->device);
+    const size_t esz_in = zt::dtype_size(dtype_in), esz_out = zt::dtype_size(dtype_out);
+    if (ndim <= 3 && zt::fused_supports_radius(radius)) {
+        // One launch for the whole box: every window clamps at the array bounds, which is what
+        // the reference's per-chunk 2r halo (clamped to the array) produces.
+        int64_t dom[3] = {1, 1, 1}, ost[3] = {0, 0, 0}, osh[3] = {1, 1, 1};
+        for (int d = 0; d < ndim; ++d) {
+            dom[3 - ndim + d] = shape[d];
+            ost[3 - ndim + d] = ostart[d];
+            osh[3 - ndim + d] = oshape[d];
+        }
+        int64_t sz = ndim == 3 ? strides[0] : 0, sy = ndim >= 2 ? strides[ndim - 2] : 0;
+        char* obase = static_cast<char*>(out) +
+                      esz_out * (ost[0] * (ndim == 3 ? sz : 0) + ost[1] * sy + ost[2]);
+        (void)esz_in;
+        int chunk_depth = ndim == 3 ? (int)chunk_shape[0] : 0;
+        return run_fused3(ctx, dtype_in, in, dom, 0, dom[0], sz, sy, ost, osh, dtype_out, obase,
+                          sz, sy, epsilon, radius, chunk_depth > 0 ? chunk_depth : 1);
+    }
+    // Separable path: chunk by chunk, each reading its 2r halo from the resident array.
+    int64_t nchunks = numel(gn, ndim);
+    int64_t ov[ZT_MAX_DIMS];
+    for (int d = 0; d < ndim; ++d) ov[d] = (int64_t)((radius * 2) & 0xFF);
+    for (int64_t c = 0; c < nchunks; ++c) {
+        int64_t rem = c, cs[ZT_MAX_DIMS], csh[ZT_MAX_DIMS];
+        for (int d = ndim - 1; d >= 0; --d) {
+            int64_t ci = g0[d] + rem % gn[d];
+            rem /= gn[d];
+            cs[d] = ci * chunk_shape[d];
+            csh[d] = std::min(cs[d] + chunk_shape[d], shape[d]) - cs[d];
+        }
+        int64_t is0[ZT_MAX_DIMS], ish[ZT_MAX_DIMS], dst[ZT_MAX_DIMS];
+        int rc = zt_subset_overlap(shape, ndim, cs, csh, ov, is0, ish, dst);
+        if (rc) return rc;
+        int64_t ioff = 0, ooff = 0;
+        for (int d = 0; d < ndim; ++d) {
+            ioff += is0[d] * strides[d];
+            ooff += cs[d] * strides[d];
+        }
+        rc = run_separable(ctx, dtype_in, static_cast<const char*>(in) + esz_in * ioff, ish,
+                           strides, ndim, dst, csh, dtype_out,
+                           static_cast<char*>(out) + esz_out * ooff, strides, epsilon, radius);
+        if (rc) return rc;
+    }
+    return ZT_OK;
+}
+
+int zt_guided_filter_apply_slab(zt_ctx* ctx, int dtype_in, const void* in, int dtype_out,
+                                void* out, const int64_t* global_shape, int64_t in_z0,
+                                int64_t in_nz, int64_t out_z0, int64_t out_nz,
+                                const int64_t* chunk_shape, float epsilon, int radius) {
+    if (int rc = check_ctx(ctx)) return rc;
+    if (int rc = dtypes_ok(dtype_in, dtype_out)) return rc;
+    if (int rc = radius_ok(radius)) return rc;
+    if (int rc = check_shape(global_shape, 3, "global_shape")) return rc;
+    if (!zt::fused_supports_radius(radius))
+        return fail(ZT_ERR_INVALID_PARAMETERS, "slab form supports radius <= %d",
+                    zt::kFusedMaxRadius);
+    const int R = radius;
+    if (in_z0 < 0 || in_nz < 0 || in_z0 + in_nz > global_shape[0] || out_z0 < in_z0 ||
+        out_z0 + out_nz > in_z0 + in_nz)
+        return fail(ZT_ERR_INVALID_PARAMETERS, "slab rows outside the array / input slab");
+    // the slab must carry the 2r halo or reach the array edge
+    if ((out_z0 - 2 * R < in_z0 && in_z0 > 0) ||
+        (out_z0 + out_nz + 2 * R > in_z0 + in_nz && in_z0 + in_nz < global_shape[0]))
+        return fail(ZT_ERR_INVALID_PARAMETERS, "input slab lacks the 2*radius halo rows");
+    if (out_nz == 0) return ZT_OK;
+    if (!in || !out) return fail(ZT_ERR_INVALID_PARAMETERS, "null data pointer");
+    DeviceGuard g(ctx->device);
+    const int64_t sy = global_shape[2], sz = global_shape[1] * global_shape[2];
+    int64_t dom[3] = {global_shape[0], global_shape[1], global_shape[2]};
+    int64_t ost[3] = {out_z0, 0, 0}, osh[3] = {out_nz, global_shape[1], global_shape[2]};
+    int depth = chunk_shape && chunk_shape[0] > 0 ? (int)chunk_shape[0] : (int)out_nz;
+    return run_fused3(ctx, dtype_in, in, dom, in_z0, in_nz, sz, sy, ost, osh, dtype_out, out, sz,
+                      sy, epsilon, radius, depth);
+}
+
+// ---- downsample ------------------------------------------------------------------------------
+
+int zt_downsample_is_compatible(int dtype_in, int dtype_out, int discrete) {
+    if (int rc = dtypes_ok(dtype_in, dtype_out)) return rc;
+    if (discrete && dtype_in >= ZT_BFLOAT16)
+        return fail(ZT_ERR_UNSUPPORTED_DATA_TYPE,
+                    "Unsupported data type %s for discrete (mode) downsampling",
+                    dtype_name(dtype_in));
+    return ZT_OK;
+}
+
+int zt_downsample_output_shape(const int64_t* in_shape, int ndim, const int64_t* stride,
+                               int64_t* out_shape) {
+    if (int rc = check_shape(in_shape, ndim, "in_shape")) return rc;
+    if (!stride || !out_shape) return fail(ZT_ERR_INVALID_PARAMETERS, "null pointer argument");
+    for (int d = 0; d < ndim; ++d) {
+        if (stride[d] <= 0) return fail(ZT_ERR_INVALID_PARAMETERS, "stride must be positive");
+        out_shape[d] = std::max<int64_t>(in_shape[d] / stride[d], 1);  // downsample.rs:162-168
+    }
+    return ZT_OK;
+}
+
+int zt_downsample_input_subset(const int64_t* in_shape, int ndim, const int64_t* stride,
+                               const int64_t* out_start, const int64_t* out_shape,
+                               int64_t* in_start, int64_t* in_subset_shape) {
+    if (int rc = check_shape(in_shape, ndim, "in_shape")) return rc;
+    if (!stride || !out_start || !out_shape || !in_start || !in_subset_shape)
+        return fail(ZT_ERR_INVALID_PARAMETERS, "null pointer argument");
+    for (int d = 0; d < ndim; ++d) {
+        if (stride[d] <= 0) return fail(ZT_ERR_INVALID_PARAMETERS, "stride must be positive");
+        // downsample.rs:65-69
+        int64_t s = out_start[d] * stride[d];
+        int64_t e = std::min((out_start[d] + out_shape[d]) * stride[d], in_shape[d]);
+        in_start[d] = s;
+        in_subset_shape[d] = std::max<int64_t>(e - s, 0);
+    }
+    return ZT_OK;
+}
+
+int zt_downsample_apply_ndarray(zt_ctx* ctx, int dtype_in, const void* in,
+                                const int64_t* in_shape, int ndim, const int64_t* stride,
+                                int discrete, int dtype_out, void* out) {
+    if (int rc = check_ctx(ctx)) return rc;
+    if (int rc = zt_downsample_is_compatible(dtype_in, dtype_out, discrete)) return rc;
+    if (int rc = check_shape(in_shape, ndim, "in_shape")) return rc;
+    if (!stride) return fail(ZT_ERR_INVALID_PARAMETERS, "null stride");
+    zt::DSParams p{};
+    p.ndim = ndim;
+    p.out_numel = 1;
+    p.win_numel = 1;
+    for (int d = 0; d < ndim; ++d) {
+        if (stride[d] <= 0) return fail(ZT_ERR_INVALID_PARAMETERS, "stride must be positive");
+        p.in_shape[d] = in_shape[d];
+        p.win[d] = std::min(stride[d], in_shape[d]);       // downsample.rs:83-85
+        p.out_shape[d] = p.win[d] > 0 ? in_shape[d] / p.win[d] : 0;  // exact_chunks
+        p.out_numel *= p.out_shape[d];
+        p.win_numel *= p.win[d];
+    }
+    if (p.out_numel == 0) return ZT_OK;
+    if (!in || !out) return fail(ZT_ERR_INVALID_PARAMETERS, "null data pointer");
+    DeviceGuard g(ctx->device);
+    if (ctx->timed) ZT_HIP(hipEventRecord(ctx->ev0, ctx->cur));
+    hipError_t e = zt::launch_downsample(in, dtype_in, out, dtype_out, p, discrete != 0, ctx->cur);
+    if (e != hipSuccess) return hip_fail(e, "downsample launch");
+    if (ctx->timed) ZT_HIP(hipEventRecord(ctx->ev1, ctx->cur));
+    return ZT_OK;
+}
+
+int zt_pyramid_level_shapes(const int64_t* shape, int ndim, const int64_t* factor, int max_levels,
+                            int64_t* level_shapes, int* n_levels) {
+    if (int rc = check_shape(shape, ndim, "shape")) return rc;
+    if (!factor || !level_shapes || !n_levels || max_levels < 0)
+        return fail(ZT_ERR_INVALID_PARAMETERS, "bad pyramid arguments");
+    int64_t cur[ZT_MAX_DIMS];
+    std::copy(shape, shape + ndim, cur);
+    int n = 0;
+    for (int i = 1; i <= max_levels; ++i) {  // zarrs_ome.rs:515
+        int64_t nxt[ZT_MAX_DIMS];
+        if (int rc = zt_downsample_output_shape(cur, ndim, factor, nxt)) return rc;
+        std::copy(nxt, nxt + ndim, level_shapes + (size_t)n * ndim);
+        ++n;
+        std::copy(nxt, nxt + ndim, cur);
+        bool stop = true;  // zarrs_ome.rs:731-737
+        for (int d = 0; d < ndim; ++d)
+            if (!(factor[d] == 1 || nxt[d] == 1)) stop = false;
+        if (stop) break;
+    }
+    *n_levels = n;
+    return ZT_OK;
+}
+
+int zt_pyramid_downsample(zt_ctx* ctx, int dtype, const void* level0, const int64_t* shape,
+                          int ndim, const int64_t* factor, int max_levels, int discrete,
+                          void* const* level_ptrs, int* levels_written) {
+    if (int rc = check_ctx(ctx)) return rc;
+    if (!level_ptrs || !levels_written) return fail(ZT_ERR_INVALID_PARAMETERS, "null pointers");
+    std::vector<int64_t> shapes((size_t)std::max(max_levels, 1) * ZT_MAX_DIMS);
+    int n = 0;
+    if (int rc = zt_pyramid_level_shapes(shape, ndim, factor, max_levels, shapes.data(), &n))
+        return rc;
+    const void* src = level0;
+    int64_t cur[ZT_MAX_DIMS];
+    std::copy(shape, shape + ndim, cur);
+    for (int i = 0; i < n; ++i) {
+        // level i+1 = downsample(level i), same dtype in/out (zarrs_ome.rs:211-234)
+        int rc = zt_downsample_apply_ndarray(ctx, dtype, src, cur, ndim, factor, discrete, dtype,
+                                             level_ptrs[i]);
+        if (rc) return rc;
+        src = level_ptrs[i];
+        std::copy(shapes.data() + (size_t)i * ndim, shapes.data() + (size_t)(i + 1) * ndim, cur);
+    }
+    *levels_written = n;
+    return ZT_OK;
+}
+
+// ---- synthetic inputs ------------------------------------------------------------------------
+
+int zt_synth_step_noise_f32(zt_ctx* ctx, float* out, const int64_t* shape, int ndim,
+                            const int64_t* global_shape, int64_t z0, uint64_t seed) {
+    if (int rc = check_ctx(ctx)) return rc;
+    if (int rc = check_shape(shape, ndim, "shape")) return rc;
+    const int64_t* gs = global_shape ? global_shape : shape;
+    int64_t n = numel(shape, ndim);
+    if (n == 0) return ZT_OK;
+    int64_t plane = n / std::max<int64_t>(shape[0], 1);
+    DeviceGuard g(ctx->device);
+    hipError_t e = zt::launch_synth_step_noise_f32(out, n, plane, shape[ndim - 1], gs[ndim - 1],
+                                                   z0, seed, ctx->cur);
+    if (e != hipSuccess) return hip_fail(e, "synth launch");
+    return ZT_OK;
+}
+
+int zt_synth_u16(zt_ctx* ctx, uint16_t* out, const int64_t* shape, int ndim,
+                 const int64_t* global_shape, int64_t z0, uint64_t seed) {
+    (void)global_shape;
+    if (int rc = check_ctx(ctx)) return rc;
+    if (int rc = check_shape(shape, ndim, "shape")) return rc;
+    int64_t n = numel(shape, ndim);
+    if (n == 0) return ZT_OK;
+    int64_t plane = n / std::max<int64_t>(shape[0], 1);
+    DeviceGuard g(ctx->device);
+    hipError_t e = zt::launch_synth_u16(out, n, plane, z0, seed, ctx->cur);
+    if (e != hipSuccess) return hip_fail(e, "synth launch");
+    return ZT_OK;
+}
+
+}  // extern "C"

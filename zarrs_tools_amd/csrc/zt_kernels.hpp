@@ -1,0 +1,79 @@
+// zt_kernels.hpp — kernel parameter blocks and launchers shared by the .hip translation units.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace zt {
+
+constexpr int kMaxDims = 8;
+constexpr int kMaxRadius = 127;         // reference: u8 radius, halo (radius*2) as u8 (guided_filter.rs:92)
+constexpr int kFusedMaxRadius = 8;      // fused 2.5-D kernel instantiations
+constexpr int kSepTreeMaxRadius = 16;   // separable path: tree sums up to here, sequential beyond
+
+// Fused 3-D guided filter. Domain = the block windows clamp to ([0,nz) x [0,ny) x [0,nx)).
+// Input element (z,y,x) lives at in + (z - in_z0)*in_sz + y*in_sy + x (x stride 1).
+// Output element (z,y,x) of the region [oz0,oz0+onz) x [oy0,..) x [ox0,..) lives at
+// out + (z-oz0)*out_sz + (y-oy0)*out_sy + (x-ox0).
+struct GFParams {
+    const void* in;
+    void* out;
+    int64_t in_sz, in_sy;
+    int64_t out_sz, out_sy;
+    int in_z0;
+    int nz, ny, nx;
+    int oz0, oy0, ox0;
+    int onz, ony, onx;
+    int zseg;  // output slices per workgroup march (normally the chunk depth)
+    int tiles_x, tiles_y, nseg;
+    float eps;
+};
+
+// N-d geometry for the separable path and downsample (C-order logical shapes).
+struct NdGeom {
+    int ndim;
+    int64_t numel;
+    int64_t shape[kMaxDims];
+    int64_t in_strides[kMaxDims];
+    int64_t out_start[kMaxDims];
+    int64_t out_shape[kMaxDims];
+    int64_t out_strides[kMaxDims];
+    int64_t out_numel;
+};
+
+bool fused_supports_radius(int radius);
+int fused_tile_y(int radius);  // output tile height of the fused kernel for this radius
+// element-type pairs with a direct fused instantiation; others are staged through f32
+bool fused_direct_pair(int dtype_in, int dtype_out);
+hipError_t launch_cast_to_f32_3d(const void* in, int dtype, int64_t sz, int64_t sy, float* out,
+                                 int64_t nz, int64_t ny, int64_t nx, hipStream_t s);
+hipError_t launch_cast_from_f32_3d(const float* in, int dtype, void* out, int64_t sz, int64_t sy,
+                                   int64_t nz, int64_t ny, int64_t nx, hipStream_t s);
+hipError_t launch_guided_fused(const GFParams& p, int dtype_in, int dtype_out, int radius,
+                               hipStream_t stream);
+// scratch must hold 5 * g.numel floats
+hipError_t launch_guided_separable(const void* in, int dtype_in, void* out, int dtype_out,
+                                   const NdGeom& g, int radius, float eps, float* scratch,
+                                   hipStream_t s);
+
+// Downsample (downsample.rs:72-120). g.shape = input shape, g.out_shape = output shape,
+// win = window per axis (min(stride, extent)).
+struct DSParams {
+    int ndim;
+    int64_t in_shape[kMaxDims];
+    int64_t out_shape[kMaxDims];
+    int64_t win[kMaxDims];
+    int64_t out_numel;
+    int64_t win_numel;
+};
+hipError_t launch_downsample(const void* in, int dtype_in, void* out, int dtype_out,
+                             const DSParams& p, bool discrete, hipStream_t s);
+
+// Synthetic inputs
+hipError_t launch_synth_step_noise_f32(float* out, int64_t n, int64_t plane, int64_t nx_row,
+                                       int64_t nx_global, int64_t z0, uint64_t seed,
+                                       hipStream_t s);
+hipError_t launch_synth_u16(uint16_t* out, int64_t n, int64_t plane, int64_t z0, uint64_t seed,
+                            hipStream_t s);
+
+}  // namespace zt
