@@ -109,7 +109,9 @@ struct RingDispatch<W, W> {
 // ---------------------------------------------------------------------------------------------
 // Sliding window sums in f64 (stage 1: the box sums of v). Sums of f32 values in f64 are exact
 // for any realistic dynamic range, so the order is immaterial and u = (f32)sum / count rounds
-// exactly like the reference's f64 summed-area-table sum (summed_area_table.rs:398-410).
+// exactly like the reference's f64 summed-area-table sum (summed_area_table.rs:398-410). That
+// matters: a = s/(s+eps) with s = (v-u)^2 is ill-conditioned in u for small eps, so u must be
+// the reference's u bit for bit.
 // ---------------------------------------------------------------------------------------------
 template <int R, int K>
 __device__ __forceinline__ void slide_sums_f64(const double (&in)[K + 2 * R], double (&out)[K]) {
@@ -125,12 +127,79 @@ __device__ __forceinline__ void slide_sums_f64(const double (&in)[K + 2 * R], do
     }
 }
 
+// s / (s + eps): rcp + one Newton step + Markstein correction (6 VALU ops instead of the ~12 of
+// IEEE division; within 1 ulp, almost always correctly rounded). Special values follow IEEE:
+// 0/0 and inf/inf give NaN as in the reference.
+__device__ __forceinline__ float fast_div(float x, float d) {
+    float y = __builtin_amdgcn_rcpf(d);
+    float e = __builtin_fmaf(-d, y, 1.0f);
+    y = __builtin_fmaf(e, y, y);
+    float q = x * y;
+    float r = __builtin_fmaf(-d, q, x);
+    return __builtin_fmaf(r, y, q);
+}
+
 // Workgroup barrier for LDS hand-offs only. __syncthreads() also fences global memory, which
-// makes the compiler drain every outstanding global load (vmcnt(0)) — including the next step's
-// prefetches this kernel keeps in flight across the barrier.
+// makes the compiler drain every outstanding global load (vmcnt(0)) — including the loads this
+// kernel keeps in flight across the barrier.
 __device__ __forceinline__ void lds_barrier() {
     __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
+template <int ABL>
+__device__ __forceinline__ void lds_barrier_abl() {
+    if constexpr (ABL & 16) __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    else lds_barrier();
+}
+
+// x / d for an integer count d given rcp = RN(1/d): Markstein's correction step makes the
+// quotient correctly rounded (checked exhaustively-by-sampling for d <= 70000, tools/README),
+// so this equals IEEE division at 3 VALU ops instead of ~11.
+__device__ __forceinline__ float div_by_count(float x, float d, float rcp) {
+    float q = x * rcp;
+    float r = __builtin_fmaf(-q, d, x);
+    return __builtin_fmaf(r, rcp, q);
+}
+
+// ---- buffer (SRD) loads/stores: 32-bit byte offsets, hardware range check (an offset past
+//      num_records reads 0 / drops the store), no 64-bit address math per access. -----------
+using rsrc_t = __amdgpu_buffer_rsrc_t;
+constexpr int kBadOff = (int)0x80000000;  // >= num_records of any slice: reads 0, writes drop
+
+__device__ __forceinline__ rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+    // Built from wave-uniform values only (T20): no waterfall loops around the buffer ops.
+    uint64_t b = (uint64_t)base;
+    uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
+    uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+    bytes = __builtin_amdgcn_readfirstlane(bytes);
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0,
+                                             (int)bytes, 0x00020000);
+}
+
+template <typename T> struct Buf;
+template <> struct Buf<float> {
+    __device__ static float load(rsrc_t r, int off) {
+        return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+    }
+    __device__ static void store(float v, rsrc_t r, int off) {
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, off, 0, 0);
+    }
+};
+template <> struct Buf<uint16_t> {
+    __device__ static float load(rsrc_t r, int off) {
+        return (float)(uint16_t)__builtin_amdgcn_raw_buffer_load_b16(r, off, 0, 0);
+    }
+    __device__ static void store(uint16_t v, rsrc_t r, int off) {
+        __builtin_amdgcn_raw_buffer_store_b16(v, r, off, 0, 0);
+    }
+};
+template <> struct Buf<uint8_t> {
+    __device__ static float load(rsrc_t r, int off) {
+        return (float)(uint8_t)__builtin_amdgcn_raw_buffer_load_b8(r, off, 0, 0);
+    }
+    __device__ static void store(uint8_t v, rsrc_t r, int off) {
+        __builtin_amdgcn_raw_buffer_store_b8(v, r, off, 0, 0);
+    }
+};
 
 // ---------------------------------------------------------------------------------------------
 // The fused kernel.
@@ -152,8 +221,9 @@ struct GFConfig {
     static constexpr int S3 = (E1Y + K3 - 1) / K3;   // segments per column, P3
     static constexpr int S4 = TX / K4;               // segments per row, P4
     static constexpr int N2 = E2Y * S2, N3 = E1X * S3, N4 = E1Y * S4;  // work items
-    static constexpr int NE2 = E2X * E2Y;
-    static constexpr int NP1 = (NE2 + NT - 1) / NT;  // apron positions per thread, P1
+    static constexpr int R1 = NT / E2X;              // P1: apron rows per pass
+    static constexpr int NP1 = (E2Y + R1 - 1) / R1;  // P1: passes (positions per thread)
+    static constexpr int W3 = W * W * W;             // interior window count
     // LDS in bytes. Region A: Lv (f64; P1 write, P2 read) aliased with La/Lb (f32; P3 write,
     // P4 read). Region B: Hx (f64; P2 write, P3 read) aliased with Ha/Hb (f32; P4 write, P5
     // read). Slack covers the over-read of the last (partial) segment.
@@ -169,15 +239,17 @@ struct GFConfig {
     static_assert(TY % K5 == 0, "ring segment must divide the tile height");
     static_assert(TX % K4 == 0, "P4 segment must divide the tile width");
     static_assert(N3 <= NT && N4 <= NT, "one P3/P4 work item per thread");
-    static_assert(NP1 <= 32, "validity mask");
+    static_assert(R1 >= 1, "P1 needs a full apron row per pass");
     static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 };
 
-template <int R, int TY, int NT, typename TIn, typename TOut>
+// ABL: ablation bits for tools/ablate.hip timing experiments only (production = 0).
+template <int R, int TY, int NT, typename TIn, typename TOut, int ABL = 0>
 __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     using C = GFConfig<R, TY, NT>;
     constexpr int TX = C::TX, W = C::W;
     constexpr int K5 = C::K5;
+    constexpr int ESZ = (int)sizeof(TIn), OSZ = (int)sizeof(TOut);
     extern __shared__ __attribute__((aligned(16))) char smem[];
     double* Lv = reinterpret_cast<double*>(smem);
     float* La = reinterpret_cast<float*>(smem);
@@ -186,17 +258,37 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     float* Ha = reinterpret_cast<float*>(smem + C::SZ_A);
     float* Hb = Ha + C::E1Y * C::PB;
 
-    const TIn* __restrict__ in = static_cast<const TIn*>(p.in);
-    TOut* __restrict__ out = static_cast<TOut*>(p.out);
-
-    // XCD-aware block -> tile: blocks b and b+8 share an XCD, so give each XCD a contiguous run
-    // of tiles (neighbouring tiles share their xy apron through that XCD's L2).
+    // XCD-aware block -> tile. Blocks b and b+8 share an XCD; give each XCD a contiguous run of
+    // logical ids and walk them in 8x4-tile super-tiles, so the WGs resident on one XCD cover a
+    // compact 512x128 region whose xy aprons and z reloads stay in that XCD's 4 MB L2.
     const int nwg = gridDim.x;
     const int b = blockIdx.x;
     const int lid = (nwg % 8 == 0) ? (b % 8) * (nwg / 8) + b / 8 : b;
-    const int tile_x = lid % p.tiles_x;
-    const int tile_y = (lid / p.tiles_x) % p.tiles_y;
-    const int seg = lid / (p.tiles_x * p.tiles_y);
+    const int ntiles = p.tiles_x * p.tiles_y;
+    const int seg = lid / ntiles;
+    int t = lid % ntiles;
+    int tile_x, tile_y;
+    {
+        const int stx = 8, sty = 4;
+        const int full_y = p.tiles_y / sty * sty;  // rows of tiles covered by full super-rows
+        const int per_srow = p.tiles_x * sty;
+        if (t < full_y * p.tiles_x) {
+            const int sr = t / per_srow, r = t % per_srow;
+            const int full_x = p.tiles_x / stx * stx;
+            if (r < full_x * sty) {
+                tile_x = (r / (stx * sty)) * stx + r % stx;
+                tile_y = sr * sty + (r / stx) % sty;
+            } else {
+                const int rr = r - full_x * sty, w = p.tiles_x - full_x;
+                tile_x = full_x + rr % w;
+                tile_y = sr * sty + rr / w;
+            }
+        } else {
+            t -= full_y * p.tiles_x;
+            tile_x = t % p.tiles_x;
+            tile_y = full_y + t / p.tiles_x;
+        }
+    }
 
     const int x0 = p.ox0 + tile_x * TX;
     const int y0 = p.oy0 + tile_y * TY;
@@ -205,117 +297,134 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     const int zo_end = min(zo_begin + p.zseg, p.oz0 + p.onz);
     const int nz = p.nz, ny = p.ny, nx = p.nx;
     const float eps = p.eps;
-    const int tid0 = threadIdx.x;
+    const uint32_t slice_bytes = (uint32_t)((int64_t)(p.ny - 1) * p.in_sy + p.nx) * ESZ;
+    const uint32_t oslice_bytes =
+        (uint32_t)((int64_t)(p.ony - 1) * p.out_sy + p.onx) * OSZ;
+    const float rcp_w3 = p.rcp_w3;  // RN(1/W^3), host-computed
 
-    auto slice_ptr = [&](int z) -> const TIn* {
-        return in + (int64_t)(z - p.in_z0) * p.in_sz;
+    const char* in_base = static_cast<const char*>(p.in);
+    auto slice_rsrc = [&](int z) -> rsrc_t {
+        const bool ok = z >= 0 && z < nz;
+        const char* base = in_base + (ok ? (int64_t)(z - p.in_z0) * p.in_sz * ESZ : 0);
+        return make_rsrc(base, ok ? slice_bytes : 0u);
     };
 
-    // ---- P1 ownership: apron positions i = tid + k*NT of the (E2X x E2Y) plane -------------
-    double zv[C::NP1];
-    int32_t poff[C::NP1];  // y*sy + x element offset within a slice (valid positions)
-    uint32_t pvalid = 0;   // bit k: position k is inside the domain
+    // ---- per-thread, step-invariant byte offsets (kBadOff where outside the domain) --------
+    const int tid0 = threadIdx.x;
+    // P1: thread -> (row0, col) of the (E2X x E2Y) apron, rows row0 + k*R1
+    int p1off[C::NP1];
+    {
+        const int row0 = tid0 / C::E2X, col = tid0 % C::E2X;
+        const int gx = x0 - 2 * R + col;
+        const bool xin = tid0 < C::R1 * C::E2X && gx >= 0 && gx < nx;
 #pragma unroll
-    for (int k = 0; k < C::NP1; ++k) {
-        int i = tid0 + k * NT;
-        int ey = i / C::E2X, ex = i % C::E2X;
-        int gy = y0 - 2 * R + ey, gx = x0 - 2 * R + ex;
-        bool ok = i < C::NE2 && gy >= 0 && gy < ny && gx >= 0 && gx < nx;
-        pvalid |= ok ? (1u << k) : 0u;
-        poff[k] = ok ? (int32_t)((int64_t)gy * p.in_sy + gx) : 0;
-        zv[k] = 0.0;
+        for (int k = 0; k < C::NP1; ++k) {
+            const int row = row0 + k * C::R1;
+            const int gy = y0 - 2 * R + row;
+            const bool ok = xin && row < C::E2Y && gy >= 0 && gy < ny;
+            p1off[k] = ok ? (int)(((int64_t)gy * p.in_sy + gx) * ESZ) : kBadOff;
+        }
     }
 
+    double zv[C::NP1];
+#pragma unroll
+    for (int k = 0; k < C::NP1; ++k) zv[k] = 0.0;
     const int zc_begin = zo_begin - R, zc_end = zo_end + R;
     const int zc0 = max(zc_begin, 0);  // first in-domain step
     // The running window advances only on in-domain steps; seed it for the first of them:
     // Zv(zc0 - 1) = sum of v over z in [zc0-1-R, zc0-1+R] clamped to [0, nz).
     {
-        int zlo = max(zc0 - 1 - R, 0), zhi = min(zc0 - 1 + R, nz - 1);
+        const int zlo = max(zc0 - 1 - R, 0), zhi = min(zc0 - 1 + R, nz - 1);
         for (int z = zlo; z <= zhi; ++z) {
-            const TIn* sp = slice_ptr(z);
+            const rsrc_t rs = slice_rsrc(z);
 #pragma unroll
-            for (int k = 0; k < C::NP1; ++k)
-                if (pvalid & (1u << k)) zv[k] += (double)Elem<TIn>::to_f32(sp[poff[k]]);
+            for (int k = 0; k < C::NP1; ++k) zv[k] += (double)Buf<TIn>::load(rs, p1off[k]);
         }
     }
-
-    // ---- prefetch registers: next step's entering/leaving slices (P1), centre slice (P3),
-    //      output slice (emit). Issued one step ahead so HBM latency hides under a step. -----
-    float pa[C::NP1], ps[C::NP1], pc3[C::K3], pv5[K5];
-    auto prefetch = [&](int zc, int tid) {
-        const int za = zc + R, zs = zc - R - 1;
-        const bool ina = zc >= 0 && zc < nz && za < nz, ins = zc >= 0 && zc < nz && zs >= 0;
-        const TIn* sa = slice_ptr(ina ? za : 0);
-        const TIn* ss = slice_ptr(ins ? zs : 0);
-#pragma unroll
-        for (int k = 0; k < C::NP1; ++k) {
-            const bool ok = (pvalid >> k) & 1u;
-            pa[k] = (ok && ina) ? Elem<TIn>::to_f32(sa[poff[k]]) : 0.0f;
-            ps[k] = (ok && ins) ? Elem<TIn>::to_f32(ss[poff[k]]) : 0.0f;
-        }
-        // P3 item of this thread: column col3, rows sg3*K3 + j of the E1 apron
-        const bool zin = zc >= 0 && zc < nz;
-        const int col3 = tid % C::E1X, sg3 = tid / C::E1X;
-        const int gx = x0 - R + col3;
-        const TIn* sc = slice_ptr(zin ? zc : 0);
-#pragma unroll
-        for (int j = 0; j < C::K3; ++j) {
-            const int gy = y0 - R + sg3 * C::K3 + j;
-            const bool ok = zin && tid < C::N3 && gx >= 0 && gx < nx && gy >= 0 && gy < ny &&
-                            sg3 * C::K3 + j < C::E1Y;
-            pc3[j] = ok ? Elem<TIn>::to_f32(sc[(int64_t)gy * p.in_sy + gx]) : 0.0f;
-        }
-        // emit: v(zo) for zo = zc - R at this thread's K5 outputs
-        const int zo = zc - R;
-        const bool zok = zo >= zo_begin && zo < zo_end;
-        const int ox = x0 + tid % TX;
-        const TIn* sv = slice_ptr(zok ? zo : zo_begin);
-#pragma unroll
-        for (int j = 0; j < K5; ++j) {
-            const int oy = y0 + (tid / TX) * K5 + j;
-            const bool ok = zok && ox < ox_end && oy < oy_end;
-            pv5[j] = ok ? Elem<TIn>::to_f32(sv[(int64_t)oy * p.in_sy + ox]) : 0.0f;
-        }
-    };
 
     float ring_a[W][K5], ring_b[W][K5];
 #pragma unroll
     for (int s = 0; s < W; ++s)
 #pragma unroll
         for (int j = 0; j < K5; ++j) ring_a[s][j] = ring_b[s][j] = 0.0f;
+    double za_run[K5], zb_run[K5];
+#pragma unroll
+    for (int j = 0; j < K5; ++j) za_run[j] = zb_run[j] = 0.0;
 
-    prefetch(zc_begin, tid0);
-    int slot = 0;
+    // P1 prefetch registers: entering slice zc+R and leaving slice zc-R-1 of the NEXT step
+    float pa[C::NP1], ps[C::NP1];
+    auto prefetch_p1 = [&](int zc) {
+        const bool zin = zc >= 0 && zc < nz;
+        const rsrc_t ra = slice_rsrc(zin ? zc + R : -1);
+        const rsrc_t rs = slice_rsrc(zin ? zc - R - 1 : -1);
+#pragma unroll
+        for (int k = 0; k < C::NP1; ++k) {
+            pa[k] = (ABL & 8) ? 1.0f : Buf<TIn>::load(ra, p1off[k]);
+            ps[k] = (ABL & 1) ? 0.5f : Buf<TIn>::load(rs, p1off[k]);
+        }
+    };
+    prefetch_p1(zc_begin);
+
     for (int zc = zc_begin; zc < zc_end; ++zc) {
-        // Launder the thread index every step so the per-phase LDS addresses are recomputed
-        // (a few VALU ops) instead of being hoisted out of the z-loop into ~40 live VGPRs.
+        // Launder the thread index every step so per-phase LDS addresses are recomputed (a few
+        // VALU ops) instead of being hoisted out of the z-loop into ~40 live VGPRs.
         int tid = threadIdx.x;
         __asm__ volatile("" : "+v"(tid));
-        // Consume this step's prefetched values, then issue the next step's loads.
-        float ca[C::NP1], cs[C::NP1], cc3[C::K3], cv5[K5];
+        const bool zin = zc >= 0 && zc < nz;
+        const int zo = zc - R;
+        const bool emit = zo >= zo_begin;
+
+        // This step's P1 inputs (loaded during the previous step) ...
+        float ca[C::NP1], cs[C::NP1];
 #pragma unroll
         for (int k = 0; k < C::NP1; ++k) { ca[k] = pa[k]; cs[k] = ps[k]; }
+        // ... then issue the loads this step itself needs later (P3 centre slice, emit slice)
+        // and the next step's P1 loads, so their latency hides under P1-P5.
+        float v3[C::K3];
+        {
+            const int col = tid % C::E1X, sg = tid / C::E1X;
+            const int gx = x0 - R + col;
+            const bool xin = tid < C::N3 && gx >= 0 && gx < nx;
+            const rsrc_t rc = slice_rsrc(zin ? zc : -1);
 #pragma unroll
-        for (int j = 0; j < C::K3; ++j) cc3[j] = pc3[j];
+            for (int j = 0; j < C::K3; ++j) {
+                const int ey = sg * C::K3 + j, gy = y0 - R + ey;
+                const bool ok = xin && ey < C::E1Y && gy >= 0 && gy < ny;
+                v3[j] = (ABL & 2) ? 1.0f
+                                  : Buf<TIn>::load(rc, ok ? (int)(((int64_t)gy * p.in_sy + gx) * ESZ)
+                                                          : kBadOff);
+            }
+        }
+        float v5[K5];
+        {
+            const int ox = x0 + tid % TX, oyb = y0 + (tid / TX) * K5;
+            const rsrc_t rv = slice_rsrc(emit ? zo : -1);
 #pragma unroll
-        for (int j = 0; j < K5; ++j) cv5[j] = pv5[j];
-        if (zc + 1 < zc_end) prefetch(zc + 1, tid);
+            for (int j = 0; j < K5; ++j) {
+                const int oy = oyb + j;
+                const bool ok = ox < ox_end && oy < oy_end;
+                v5[j] = (ABL & 4) ? 1.0f
+                                  : Buf<TIn>::load(rv, ok ? (int)(((int64_t)oy * p.in_sy + ox) * ESZ)
+                                                          : kBadOff);
+            }
+        }
+        if (zc + 1 < zc_end) prefetch_p1(zc + 1);
 
         float s2a[K5], s2b[K5];
-        if (zc >= 0 && zc < nz) {
+        if (zin) {
             // ---- P1: running z-window of v (f64) on the E2 apron -> Lv ----------------------
+            {
+                const int row0 = tid / C::E2X, col = tid % C::E2X;
+                double* dst = Lv + row0 * C::PV + col;
+                const bool act = tid < C::R1 * C::E2X;
 #pragma unroll
-            for (int k = 0; k < C::NP1; ++k) {
-                zv[k] = zv[k] + (double)ca[k];  // entering slice zc+R (0 when outside)
-                zv[k] = zv[k] - (double)cs[k];  // leaving slice zc-R-1 (0 when outside)
-                const int i = tid + k * NT;
-                if (i < C::NE2) {
-                    const int ey = i / C::E2X, ex = i % C::E2X;
-                    Lv[ey * C::PV + ex] = zv[k];
+                for (int k = 0; k < C::NP1; ++k) {
+                    zv[k] = zv[k] + (double)ca[k];  // entering slice zc+R (0 outside)
+                    zv[k] = zv[k] - (double)cs[k];  // leaving slice zc-R-1 (0 outside)
+                    if (act && row0 + k * C::R1 < C::E2Y) dst[k * C::R1 * C::PV] = zv[k];
                 }
             }
-            lds_barrier();
+            lds_barrier_abl<ABL>();
             // ---- P2: x-window sums (f64) of Lv rows -> Hx (E2Y rows x E1X cols) -------------
 #pragma unroll 1
             for (int item = tid; item < C::N2; item += NT) {
@@ -325,11 +434,12 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
 #pragma unroll
                 for (int j = 0; j < C::K2 + 2 * R; ++j) vin[j] = src[j];
                 slide_sums_f64<R, C::K2>(vin, vout);
+                double* dst = Hx + row * C::PH + sg * C::K2;
 #pragma unroll
                 for (int j = 0; j < C::K2; ++j)
-                    if (sg * C::K2 + j < C::E1X) Hx[row * C::PH + sg * C::K2 + j] = vout[j];
+                    if (sg * C::K2 + j < C::E1X) dst[j] = vout[j];
             }
-            lds_barrier();
+            lds_barrier_abl<ABL>();
             // ---- P3: y-window sums (f64) of Hx columns -> U on E1; pointwise a, b -----------
             if (tid < C::N3) {
                 const int col = tid % C::E1X, sg = tid / C::E1X;
@@ -340,28 +450,35 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
                 slide_sums_f64<R, C::K3>(vin, U);
                 const int gx = x0 - R + col;
                 const bool xin = gx >= 0 && gx < nx;
-                const int cxz = xin ? clamped_count(gx, nx, R) * clamped_count(zc, nz, R) : 1;
+                const int cxz = clamped_count(gx, nx, R) * clamped_count(zc, nz, R);
 #pragma unroll
                 for (int j = 0; j < C::K3; ++j) {
                     const int ey = sg * C::K3 + j;
                     const int gy = y0 - R + ey;
-                    float a = 0.0f, bb = 0.0f;
-                    if (ey < C::E1Y && xin && gy >= 0 && gy < ny) {
-                        // summed_area_table_mean: (sum as f32) / (count as f32)
-                        const float cnt = (float)(clamped_count(gy, ny, R) * cxz);
-                        const float u = (float)U[j] / cnt;
-                        const float d = cc3[j] - u;
-                        const float s = d * d;       // (v - u).powf(2.0)
-                        a = s / (s + eps);
+                    // summed_area_table_mean: (sum as f32) / (count as f32)
+                    const int cnt = clamped_count(gy, ny, R) * cxz;
+                    const float fc = (float)cnt;
+                    const float rc = cnt == C::W3 ? rcp_w3 : 1.0f / fc;
+                    const float u = div_by_count((float)U[j], fc, rc);
+                    const float d = v3[j] - u;
+                    const float s = d * d;  // (v - u).powf(2.0)
+                    float a, bb;
+                    if constexpr (ABL & 32) {
+                        a = s; bb = u;
+                    } else {
+                        a = fast_div(s, s + eps);
                         bb = (1.0f - a) * u;
                     }
+                    const bool ok = xin && gy >= 0 && gy < ny;
+                    a = ok ? a : 0.0f;  // zero outside the domain: the clamped window sum
+                    bb = ok ? bb : 0.0f;
                     if (ey < C::E1Y) {
                         La[ey * C::PA + col] = a;
                         Lb[ey * C::PA + col] = bb;
                     }
                 }
             }
-            lds_barrier();
+            lds_barrier_abl<ABL>();
             // ---- P4: x-window sums of La/Lb rows -> Ha/Hb (E1Y rows x TX cols) --------------
             if (tid < C::N4) {
                 const int row = tid % C::E1Y, sg = tid / C::E1Y;
@@ -384,7 +501,7 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
                     for (int j = 0; j < C::K4; ++j) Hb[row * C::PB + sg * C::K4 + j] = vout[j];
                 }
             }
-            lds_barrier();
+            lds_barrier_abl<ABL>();
             // ---- P5: y-window sums of Ha/Hb columns -> this slice's tile sums ---------------
             {
                 const int col5 = tid % TX, seg5 = tid / TX;
@@ -403,45 +520,55 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
             for (int j = 0; j < K5; ++j) s2a[j] = s2b[j] = 0.0f;
         }
 
-        // ---- ring update; z-window sums (oldest -> newest) for zo = zc - R ------------------
-        const int zo = zc - R;
-        float A[K5], B[K5];
-        RingDispatch<0, W>::run(slot, [&](auto slot_c) {
-            constexpr int SL = decltype(slot_c)::value;
+        // ---- ring: the z-window of the slice sums as an exact (f64) running sum, the ring
+        //      only supplies the value leaving the window. ----------------------------------
+        float olda[K5], oldb[K5];
+        // FIFO of the last W slice sums: read the leaving (oldest) entry, shift, append.
+        // A shift register keeps every index static (a runtime slot index would push the ring
+        // to scratch memory); it costs (W-1) moves per entry, no branches.
 #pragma unroll
-            for (int j = 0; j < K5; ++j) {
-                ring_a[SL][j] = s2a[j];
-                ring_b[SL][j] = s2b[j];
-                float za[W], zb[W];
+        for (int j = 0; j < K5; ++j) {
+            olda[j] = ring_a[0][j];
+            oldb[j] = ring_b[0][j];
 #pragma unroll
-                for (int t = 0; t < W; ++t) {
-                    za[t] = ring_a[(SL + 1 + t) % W][j];
-                    zb[t] = ring_b[(SL + 1 + t) % W][j];
-                }
-                float sa[1], sb[1];
-                tree_window_sums<R, 1>(za, sa);
-                tree_window_sums<R, 1>(zb, sb);
-                A[j] = sa[0];
-                B[j] = sb[0];
+            for (int t2 = 0; t2 + 1 < W; ++t2) {
+                ring_a[t2][j] = ring_a[t2 + 1][j];
+                ring_b[t2][j] = ring_b[t2 + 1][j];
             }
-        });
-        const int ox5 = x0 + tid % TX;
-        if (zo >= zo_begin && ox5 < ox_end) {
-            const int cxz = clamped_count(ox5, nx, R) * clamped_count(zo, nz, R);
-            TOut* po = out + (int64_t)(zo - p.oz0) * p.out_sz;
+            ring_a[W - 1][j] = s2a[j];
+            ring_b[W - 1][j] = s2b[j];
+        }
+        float A[K5], B[K5];
+#pragma unroll
+        for (int j = 0; j < K5; ++j) {
+            za_run[j] = za_run[j] + (double)s2a[j];
+            za_run[j] = za_run[j] - (double)olda[j];
+            zb_run[j] = zb_run[j] + (double)s2b[j];
+            zb_run[j] = zb_run[j] - (double)oldb[j];
+            A[j] = (float)za_run[j];
+            B[j] = (float)zb_run[j];
+        }
+        if (emit) {
+            const int ox = x0 + tid % TX, oyb = y0 + (tid / TX) * K5;
+            const int cxz = clamped_count(ox, nx, R) * clamped_count(zo, nz, R);
+            const char* obase = static_cast<const char*>(p.out) +
+                                (int64_t)(zo - p.oz0) * p.out_sz * OSZ;
+            const rsrc_t ro = make_rsrc(obase, oslice_bytes);
 #pragma unroll
             for (int j = 0; j < K5; ++j) {
-                const int oy = y0 + (tid / TX) * K5 + j;
-                if (oy < oy_end) {
-                    const float cnt = (float)(clamped_count(oy, ny, R) * cxz);
-                    const float ma = A[j] / cnt;
-                    const float mb = B[j] / cnt;
-                    const float o = __fadd_rn(__fmul_rn(cv5[j], ma), mb);  // v *= ma; v += mb
-                    po[(int64_t)(oy - p.oy0) * p.out_sy + (ox5 - p.ox0)] = from_f32<TOut>(o);
-                }
+                const int oy = oyb + j;
+                const int cnt = clamped_count(oy, ny, R) * cxz;
+                const float fc = (float)cnt;
+                const float rc = cnt == C::W3 ? rcp_w3 : 1.0f / fc;
+                const float ma = div_by_count(A[j], fc, rc);
+                const float mb = div_by_count(B[j], fc, rc);
+                const float o = __fadd_rn(__fmul_rn(v5[j], ma), mb);  // v *= ma; v += mb
+                const bool ok = ox < ox_end && oy < oy_end;
+                const int off =
+                    ok ? (int)(((int64_t)(oy - p.oy0) * p.out_sy + (ox - p.ox0)) * OSZ) : kBadOff;
+                Buf<TOut>::store(from_f32<TOut>(o), ro, off);
             }
         }
-        slot = slot + 1 == W ? 0 : slot + 1;
     }
 }
 
@@ -452,6 +579,11 @@ template <int R, int TY, int NT, typename TIn, typename TOut>
 inline hipError_t launch_fused_cfg(const GFParams& p0, hipStream_t stream) {
     using C = GFConfig<R, TY, NT>;
     GFParams p = p0;
+    {
+        const float w3 = (float)(C::W3);
+        volatile float one = 1.0f;  // IEEE division on the host: RN(1/W^3)
+        p.rcp_w3 = one / w3;
+    }
     p.tiles_x = (p.onx + C::TX - 1) / C::TX;
     p.tiles_y = (p.ony + TY - 1) / TY;
     p.nseg = (p.onz + p.zseg - 1) / p.zseg;

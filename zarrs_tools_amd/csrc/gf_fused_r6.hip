@@ -2,5 +2,5 @@
 #include "gf_fused.hpp"
 
 namespace zt {
-ZT_FUSED_PAIRS(6, 32, 1024)
+ZT_FUSED_PAIRS(6, 16, 1024)
 }  // namespace zt

@@ -2,5 +2,5 @@
 #include "gf_fused.hpp"
 
 namespace zt {
-ZT_FUSED_PAIRS(8, 32, 1024)
+ZT_FUSED_PAIRS(8, 16, 1024)
 }  // namespace zt

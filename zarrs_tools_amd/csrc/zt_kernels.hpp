@@ -27,6 +27,7 @@ struct GFParams {
     int zseg;  // output slices per workgroup march (normally the chunk depth)
     int tiles_x, tiles_y, nseg;
     float eps;
+    float rcp_w3;  // RN(1 / (2r+1)^3): the interior window count's reciprocal (host-computed)
 };
 
 // N-d geometry for the separable path and downsample (C-order logical shapes).
