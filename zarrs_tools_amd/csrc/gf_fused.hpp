@@ -83,10 +83,70 @@ __device__ __forceinline__ void tree_window_sums(const float (&in)[K + 2 * R], f
     }
 }
 
+// Generic version for vector element types (float2 = the (a, b) pair of stage 2).
+template <int R, int K, typename T>
+__device__ __forceinline__ void tree_window_sums_t(const T (&in)[K + 2 * R], T (&out)[K]) {
+    constexpr int W = 2 * R + 1;
+    constexpr int N = K + 2 * R;
+    if constexpr (W == 1) {
+#pragma unroll
+        for (int i = 0; i < K; ++i) out[i] = in[i];
+    } else {
+        T p2[N], p4[N], p8[N], p16[N];
+#pragma unroll
+        for (int i = 0; i + 1 < N; ++i) p2[i] = in[i] + in[i + 1];
+        if constexpr (W >= 4) {
+#pragma unroll
+            for (int i = 0; i + 3 < N; ++i) p4[i] = p2[i] + p2[i + 2];
+        }
+        if constexpr (W >= 8) {
+#pragma unroll
+            for (int i = 0; i + 7 < N; ++i) p8[i] = p4[i] + p4[i + 4];
+        }
+        if constexpr (W >= 16) {
+#pragma unroll
+            for (int i = 0; i + 15 < N; ++i) p16[i] = p8[i] + p8[i + 8];
+        }
+        static_assert(W < 32, "fused radii only");
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+            T acc{};
+            int off = 0;
+            bool first = true;
+#pragma unroll
+            for (int b = 4; b >= 0; --b) {
+                if (W & (1 << b)) {
+                    T piece;
+                    switch (b) {
+                    case 0: piece = in[i + off]; break;
+                    case 1: piece = p2[i + off]; break;
+                    case 2: piece = p4[i + off]; break;
+                    case 3: piece = p8[i + off]; break;
+                    default: piece = p16[i + off]; break;
+                    }
+                    acc = first ? piece : acc + piece;
+                    first = false;
+                    off += 1 << b;
+                }
+            }
+            out[i] = acc;
+        }
+    }
+}
+
 __device__ __forceinline__ int clamped_count(int i, int n, int r) {
     int lo = i - r < 0 ? 0 : i - r;
     int hi = i + r > n - 1 ? n - 1 : i + r;
     return hi - lo + 1;
+}
+
+// Compile-time loop: f(integral_constant<I>) for I in [B, E).
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        static_for<B + 1, E>(f);
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -203,6 +263,14 @@ template <> struct Buf<uint8_t> {
 
 // ---------------------------------------------------------------------------------------------
 // The fused kernel.
+//
+// Software-pipelined phases, two LDS barriers per z-step. Iteration `i` runs
+//   C0: P3(i)  [U -> a,b on the E1 apron]  +  P1(i+1) [z-window of v]  +  P5(i-1) [y-sums,
+//       z-ring, emit out(i-1-R)]
+//   C1: P4(i)  [x-sums of (a,b)]           +  P2(i+1) [x-sums of the v z-window]
+// with separate LDS buffers per hand-off (Lv, Hx, Lab, Hab), so each barrier interval holds
+// independent work from different slices (better wave balance, half the barriers of a
+// straight P1..P5 sequence).
 // ---------------------------------------------------------------------------------------------
 template <int R, int TY, int NT>
 struct GFConfig {
@@ -210,11 +278,13 @@ struct GFConfig {
     static constexpr int W = 2 * R + 1;
     static constexpr int E2X = TX + 4 * R, E2Y = TY + 4 * R;  // v / Zv apron
     static constexpr int E1X = TX + 2 * R, E1Y = TY + 2 * R;  // u / a / b apron
-    static constexpr int odd(int x) { return (x & 1) ? x : x + 1; }
-    static constexpr int PV = odd(E2X);   // Lv pitch (f64)  x-pass reads rows, lane <-> row
-    static constexpr int PH = odd(E1X);   // Hx pitch (f64)  x-pass writes rows, lane <-> row
-    static constexpr int PA = odd(E1X);   // La/Lb pitch (f32)
-    static constexpr int PB = odd(TX);    // Ha/Hb pitch (f32)
+    // Pitches in 8-byte elements, = 2 mod 4: 16-B aligned rows and conflict-free ds_*_b128
+    // when lanes walk rows (16-lane groups land on distinct 4-bank slots).
+    static constexpr int p2m4(int x) { return x + ((2 - x % 4) + 4) % 4; }
+    static constexpr int PV = p2m4(E2X);  // Lv  (f64)    P1 writes, P2 reads rows
+    static constexpr int PH = p2m4(E1X);  // Hx  (f64)    P2 writes rows, P3 reads columns
+    static constexpr int PA = p2m4(E1X);  // Lab (float2) P3 writes, P4 reads rows
+    static constexpr int PB = p2m4(TX);   // Hab (float2) P4 writes rows, P5 reads columns
     static constexpr int K2 = 4, K3 = 4, K4 = 4;
     static constexpr int K5 = TX * TY / NT;          // outputs per thread (ring width)
     static constexpr int S2 = (E1X + K2 - 1) / K2;   // segments per row, P2
@@ -224,26 +294,26 @@ struct GFConfig {
     static constexpr int R1 = NT / E2X;              // P1: apron rows per pass
     static constexpr int NP1 = (E2Y + R1 - 1) / R1;  // P1: passes (positions per thread)
     static constexpr int W3 = W * W * W;             // interior window count
-    // LDS in bytes. Region A: Lv (f64; P1 write, P2 read) aliased with La/Lb (f32; P3 write,
-    // P4 read). Region B: Hx (f64; P2 write, P3 read) aliased with Ha/Hb (f32; P4 write, P5
-    // read). Slack covers the over-read of the last (partial) segment.
-    static constexpr int SLACK = 16 * 1024;
-    static constexpr int SZ_LV = E2Y * PV * 8;
-    static constexpr int SZ_LAB = 2 * E1Y * PA * 4;
-    static constexpr int SZ_A = ((SZ_LV > SZ_LAB ? SZ_LV : SZ_LAB) + SLACK + 15) / 16 * 16;
-    static constexpr int SZ_HX = E2Y * PH * 8;
-    static constexpr int SZ_HAB = 2 * E1Y * PB * 4;
-    static constexpr int SZ_B = ((SZ_HX > SZ_HAB ? SZ_HX : SZ_HAB) + SLACK + 15) / 16 * 16;
-    static constexpr int LDS_BYTES = SZ_A + SZ_B;
+    static constexpr int al(int b) { return (b + 255) / 256 * 256; }
+    static constexpr int SZ_LV = al((E2Y + 1) * PV * 8);
+    static constexpr int SZ_HX = al((E2Y + K3) * PH * 8);
+    static constexpr int SZ_LAB = al((E1Y + 1) * PA * 8);
+    static constexpr int SZ_HAB = al((E1Y + 1) * PB * 8);
+    static constexpr int OFF_HX = SZ_LV, OFF_LAB = OFF_HX + SZ_HX, OFF_HAB = OFF_LAB + SZ_LAB;
+    static constexpr int OFF_RCP = OFF_HAB + SZ_HAB;
+    static constexpr int SZ_RCP = al((W3 + 1) * 4);  // RN(1/c) for window counts c <= W^3
+    static constexpr int LDS_BYTES = OFF_RCP + SZ_RCP;
+    // item -> thread placement: heavy phases on different waves (see C0 / C1)
+    static constexpr int T3 = NT - N3;  // P3 items on the top threads
+    static constexpr int T2 = NT - N2;  // P2 items on the top threads, P4 on the bottom
     static_assert(TX * TY % NT == 0, "tile must divide evenly over the threads");
     static_assert(TY % K5 == 0, "ring segment must divide the tile height");
     static_assert(TX % K4 == 0, "P4 segment must divide the tile width");
-    static_assert(N3 <= NT && N4 <= NT, "one P3/P4 work item per thread");
+    static_assert(N2 <= NT && N3 <= NT && N4 <= NT, "one work item per thread per phase");
     static_assert(R1 >= 1, "P1 needs a full apron row per pass");
     static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 };
 
-// ABL: ablation bits for tools/ablate.hip timing experiments only (production = 0).
 template <int R, int TY, int NT, typename TIn, typename TOut, int ABL = 0>
 __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     using C = GFConfig<R, TY, NT>;
@@ -252,11 +322,13 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     constexpr int ESZ = (int)sizeof(TIn), OSZ = (int)sizeof(TOut);
     extern __shared__ __attribute__((aligned(16))) char smem[];
     double* Lv = reinterpret_cast<double*>(smem);
-    float* La = reinterpret_cast<float*>(smem);
-    float* Lb = La + C::E1Y * C::PA;
-    double* Hx = reinterpret_cast<double*>(smem + C::SZ_A);
-    float* Ha = reinterpret_cast<float*>(smem + C::SZ_A);
-    float* Hb = Ha + C::E1Y * C::PB;
+    double* Hx = reinterpret_cast<double*>(smem + C::OFF_HX);
+    float2* Lab = reinterpret_cast<float2*>(smem + C::OFF_LAB);
+    float2* Hab = reinterpret_cast<float2*>(smem + C::OFF_HAB);
+    float* rcp_tab = reinterpret_cast<float*>(smem + C::OFF_RCP);
+    // Correctly rounded reciprocals of every possible window count, for div_by_count
+    // (Markstein's correction needs RN(1/c) exactly). Published by the prologue's barriers.
+    for (int c = threadIdx.x; c <= C::W3; c += NT) rcp_tab[c] = c > 0 ? 1.0f / (float)c : 0.0f;
 
     // XCD-aware block -> tile. Blocks b and b+8 share an XCD; give each XCD a contiguous run of
     // logical ids and walk them in 8x4-tile super-tiles, so the WGs resident on one XCD cover a
@@ -270,7 +342,7 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     int tile_x, tile_y;
     {
         const int stx = 8, sty = 4;
-        const int full_y = p.tiles_y / sty * sty;  // rows of tiles covered by full super-rows
+        const int full_y = p.tiles_y / sty * sty;
         const int per_srow = p.tiles_x * sty;
         if (t < full_y * p.tiles_x) {
             const int sr = t / per_srow, r = t % per_srow;
@@ -300,7 +372,7 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     const uint32_t slice_bytes = (uint32_t)((int64_t)(p.ny - 1) * p.in_sy + p.nx) * ESZ;
     const uint32_t oslice_bytes =
         (uint32_t)((int64_t)(p.ony - 1) * p.out_sy + p.onx) * OSZ;
-    const float rcp_w3 = p.rcp_w3;  // RN(1/W^3), host-computed
+    const int sy = (int)p.in_sy, osy = (int)p.out_sy;  // 32-bit: slices < 2 GiB (host check)
 
     const char* in_base = static_cast<const char*>(p.in);
     auto slice_rsrc = [&](int z) -> rsrc_t {
@@ -311,7 +383,6 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
 
     // ---- per-thread, step-invariant byte offsets (kBadOff where outside the domain) --------
     const int tid0 = threadIdx.x;
-    // P1: thread -> (row0, col) of the (E2X x E2Y) apron, rows row0 + k*R1
     int p1off[C::NP1];
     {
         const int row0 = tid0 / C::E2X, col = tid0 % C::E2X;
@@ -322,19 +393,19 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
             const int row = row0 + k * C::R1;
             const int gy = y0 - 2 * R + row;
             const bool ok = xin && row < C::E2Y && gy >= 0 && gy < ny;
-            p1off[k] = ok ? (int)(((int64_t)gy * p.in_sy + gx) * ESZ) : kBadOff;
+            p1off[k] = ok ? (gy * sy + gx) * ESZ : kBadOff;
         }
     }
 
     double zv[C::NP1];
 #pragma unroll
     for (int k = 0; k < C::NP1; ++k) zv[k] = 0.0;
-    const int zc_begin = zo_begin - R, zc_end = zo_end + R;
-    const int zc0 = max(zc_begin, 0);  // first in-domain step
-    // The running window advances only on in-domain steps; seed it for the first of them:
-    // Zv(zc0 - 1) = sum of v over z in [zc0-1-R, zc0-1+R] clamped to [0, nz).
+    const int zc_begin = zo_begin - R, zc_end = zo_end + R;  // stage-1 slices of this march
+    // Running z-window: seed Zv(zc_begin - 1) = sum of v over [zc_begin-1-R, zc_begin-1+R]
+    // clamped to [0, nz); every later step adds the entering and subtracts the leaving slice
+    // (both 0 outside the domain), so the window stays exact through out-of-domain steps.
     {
-        const int zlo = max(zc0 - 1 - R, 0), zhi = min(zc0 - 1 + R, nz - 1);
+        const int zlo = max(zc_begin - 1 - R, 0), zhi = min(zc_begin - 1 + R, nz - 1);
         for (int z = zlo; z <= zhi; ++z) {
             const rsrc_t rs = slice_rsrc(z);
 #pragma unroll
@@ -351,205 +422,156 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
 #pragma unroll
     for (int j = 0; j < K5; ++j) za_run[j] = zb_run[j] = 0.0;
 
-    // P1 prefetch registers: entering slice zc+R and leaving slice zc-R-1 of the NEXT step
-    float pa[C::NP1], ps[C::NP1];
-    auto prefetch_p1 = [&](int zc) {
-        const bool zin = zc >= 0 && zc < nz;
-        const rsrc_t ra = slice_rsrc(zin ? zc + R : -1);
-        const rsrc_t rs = slice_rsrc(zin ? zc - R - 1 : -1);
+    // ---- phase bodies ----------------------------------------------------------------------
+    float pa[C::NP1], ps[C::NP1];  // P1 inputs for the next stage-1 slice (prefetched)
+    auto load_p1 = [&](int zc) {    // entering slice zc+R and leaving slice zc-R-1 of step zc
+        const rsrc_t ra = slice_rsrc(zc + R);
+        const rsrc_t rs = slice_rsrc(zc - R - 1);
 #pragma unroll
         for (int k = 0; k < C::NP1; ++k) {
             pa[k] = (ABL & 8) ? 1.0f : Buf<TIn>::load(ra, p1off[k]);
             ps[k] = (ABL & 1) ? 0.5f : Buf<TIn>::load(rs, p1off[k]);
         }
     };
-    prefetch_p1(zc_begin);
-
-    for (int zc = zc_begin; zc < zc_end; ++zc) {
-        // Launder the thread index every step so per-phase LDS addresses are recomputed (a few
-        // VALU ops) instead of being hoisted out of the z-loop into ~40 live VGPRs.
-        int tid = threadIdx.x;
-        __asm__ volatile("" : "+v"(tid));
-        const bool zin = zc >= 0 && zc < nz;
-        const int zo = zc - R;
-        const bool emit = zo >= zo_begin;
-
-        // This step's P1 inputs (loaded during the previous step) ...
-        float ca[C::NP1], cs[C::NP1];
+    auto do_p1 = [&](int tid) {  // z-window of v (f64) on the E2 apron -> Lv
+        const int row0 = tid / C::E2X, col = tid % C::E2X;
+        double* dst = Lv + row0 * C::PV + col;
+        const bool act = tid < C::R1 * C::E2X;
 #pragma unroll
-        for (int k = 0; k < C::NP1; ++k) { ca[k] = pa[k]; cs[k] = ps[k]; }
-        // ... then issue the loads this step itself needs later (P3 centre slice, emit slice)
-        // and the next step's P1 loads, so their latency hides under P1-P5.
-        float v3[C::K3];
-        {
-            const int col = tid % C::E1X, sg = tid / C::E1X;
-            const int gx = x0 - R + col;
-            const bool xin = tid < C::N3 && gx >= 0 && gx < nx;
-            const rsrc_t rc = slice_rsrc(zin ? zc : -1);
-#pragma unroll
-            for (int j = 0; j < C::K3; ++j) {
-                const int ey = sg * C::K3 + j, gy = y0 - R + ey;
-                const bool ok = xin && ey < C::E1Y && gy >= 0 && gy < ny;
-                v3[j] = (ABL & 2) ? 1.0f
-                                  : Buf<TIn>::load(rc, ok ? (int)(((int64_t)gy * p.in_sy + gx) * ESZ)
-                                                          : kBadOff);
-            }
+        for (int k = 0; k < C::NP1; ++k) {
+            zv[k] = zv[k] + (double)pa[k];  // entering slice zc+R (0 outside the domain)
+            zv[k] = zv[k] - (double)ps[k];  // leaving slice zc-R-1 (0 outside the domain)
+            if (act && row0 + k * C::R1 < C::E2Y) dst[k * C::R1 * C::PV] = zv[k];
         }
-        float v5[K5];
-        {
-            const int ox = x0 + tid % TX, oyb = y0 + (tid / TX) * K5;
-            const rsrc_t rv = slice_rsrc(emit ? zo : -1);
+    };
+    auto do_p2 = [&](int tid) {  // x-window sums (f64) of Lv rows -> Hx
+        const int item = tid - C::T2;
+        if (item < 0) return;
+        const int row = item % C::E2Y, sg = item / C::E2Y;
+        const double2* src =
+            reinterpret_cast<const double2*>(Lv + row * C::PV + sg * C::K2);
+        double vin[C::K2 + 2 * R], vout[C::K2];
 #pragma unroll
-            for (int j = 0; j < K5; ++j) {
-                const int oy = oyb + j;
-                const bool ok = ox < ox_end && oy < oy_end;
-                v5[j] = (ABL & 4) ? 1.0f
-                                  : Buf<TIn>::load(rv, ok ? (int)(((int64_t)oy * p.in_sy + ox) * ESZ)
-                                                          : kBadOff);
-            }
+        for (int j = 0; j < (C::K2 + 2 * R) / 2; ++j) {
+            const double2 d2 = src[j];
+            vin[2 * j] = d2.x;
+            vin[2 * j + 1] = d2.y;
         }
-        if (zc + 1 < zc_end) prefetch_p1(zc + 1);
-
-        float s2a[K5], s2b[K5];
-        if (zin) {
-            // ---- P1: running z-window of v (f64) on the E2 apron -> Lv ----------------------
-            {
-                const int row0 = tid / C::E2X, col = tid % C::E2X;
-                double* dst = Lv + row0 * C::PV + col;
-                const bool act = tid < C::R1 * C::E2X;
+        if constexpr ((C::K2 + 2 * R) % 2) vin[C::K2 + 2 * R - 1] = Lv[row * C::PV + sg * C::K2 + C::K2 + 2 * R - 1];
+        slide_sums_f64<R, C::K2>(vin, vout);
+        double2* dst = reinterpret_cast<double2*>(Hx + row * C::PH + sg * C::K2);
 #pragma unroll
-                for (int k = 0; k < C::NP1; ++k) {
-                    zv[k] = zv[k] + (double)ca[k];  // entering slice zc+R (0 outside)
-                    zv[k] = zv[k] - (double)cs[k];  // leaving slice zc-R-1 (0 outside)
-                    if (act && row0 + k * C::R1 < C::E2Y) dst[k * C::R1 * C::PV] = zv[k];
-                }
-            }
-            lds_barrier_abl<ABL>();
-            // ---- P2: x-window sums (f64) of Lv rows -> Hx (E2Y rows x E1X cols) -------------
-#pragma unroll 1
-            for (int item = tid; item < C::N2; item += NT) {
-                const int row = item % C::E2Y, sg = item / C::E2Y;
-                const double* src = Lv + row * C::PV + sg * C::K2;
-                double vin[C::K2 + 2 * R], vout[C::K2];
+        for (int j = 0; j < C::K2 / 2; ++j)
+            if (sg * C::K2 + 2 * j < C::E1X) dst[j] = make_double2(vout[2 * j], vout[2 * j + 1]);
+    };
+    float v3[C::K3];  // v at the P3 item's E1 positions, slice i (prefetched one step ahead)
+    auto load_v3 = [&](int tid, int zc) {
+        const int item = tid - C::T3;
+        const int col = item % C::E1X, sg = item / C::E1X;
+        const int gx = x0 - R + col;
+        const bool xin = item >= 0 && gx >= 0 && gx < nx;
+        const rsrc_t rc = slice_rsrc(zc);
 #pragma unroll
-                for (int j = 0; j < C::K2 + 2 * R; ++j) vin[j] = src[j];
-                slide_sums_f64<R, C::K2>(vin, vout);
-                double* dst = Hx + row * C::PH + sg * C::K2;
-#pragma unroll
-                for (int j = 0; j < C::K2; ++j)
-                    if (sg * C::K2 + j < C::E1X) dst[j] = vout[j];
-            }
-            lds_barrier_abl<ABL>();
-            // ---- P3: y-window sums (f64) of Hx columns -> U on E1; pointwise a, b -----------
-            if (tid < C::N3) {
-                const int col = tid % C::E1X, sg = tid / C::E1X;
-                const double* src = Hx + (sg * C::K3) * C::PH + col;
-                double vin[C::K3 + 2 * R], U[C::K3];
-#pragma unroll
-                for (int j = 0; j < C::K3 + 2 * R; ++j) vin[j] = src[j * C::PH];
-                slide_sums_f64<R, C::K3>(vin, U);
-                const int gx = x0 - R + col;
-                const bool xin = gx >= 0 && gx < nx;
-                const int cxz = clamped_count(gx, nx, R) * clamped_count(zc, nz, R);
-#pragma unroll
-                for (int j = 0; j < C::K3; ++j) {
-                    const int ey = sg * C::K3 + j;
-                    const int gy = y0 - R + ey;
-                    // summed_area_table_mean: (sum as f32) / (count as f32)
-                    const int cnt = clamped_count(gy, ny, R) * cxz;
-                    const float fc = (float)cnt;
-                    const float rc = cnt == C::W3 ? rcp_w3 : 1.0f / fc;
-                    const float u = div_by_count((float)U[j], fc, rc);
-                    const float d = v3[j] - u;
-                    const float s = d * d;  // (v - u).powf(2.0)
-                    float a, bb;
-                    if constexpr (ABL & 32) {
-                        a = s; bb = u;
-                    } else {
-                        a = fast_div(s, s + eps);
-                        bb = (1.0f - a) * u;
-                    }
-                    const bool ok = xin && gy >= 0 && gy < ny;
-                    a = ok ? a : 0.0f;  // zero outside the domain: the clamped window sum
-                    bb = ok ? bb : 0.0f;
-                    if (ey < C::E1Y) {
-                        La[ey * C::PA + col] = a;
-                        Lb[ey * C::PA + col] = bb;
-                    }
-                }
-            }
-            lds_barrier_abl<ABL>();
-            // ---- P4: x-window sums of La/Lb rows -> Ha/Hb (E1Y rows x TX cols) --------------
-            if (tid < C::N4) {
-                const int row = tid % C::E1Y, sg = tid / C::E1Y;
-                {
-                    const float* src = La + row * C::PA + sg * C::K4;
-                    float vin[C::K4 + 2 * R], vout[C::K4];
-#pragma unroll
-                    for (int j = 0; j < C::K4 + 2 * R; ++j) vin[j] = src[j];
-                    tree_window_sums<R, C::K4>(vin, vout);
-#pragma unroll
-                    for (int j = 0; j < C::K4; ++j) Ha[row * C::PB + sg * C::K4 + j] = vout[j];
-                }
-                {
-                    const float* src = Lb + row * C::PA + sg * C::K4;
-                    float vin[C::K4 + 2 * R], vout[C::K4];
-#pragma unroll
-                    for (int j = 0; j < C::K4 + 2 * R; ++j) vin[j] = src[j];
-                    tree_window_sums<R, C::K4>(vin, vout);
-#pragma unroll
-                    for (int j = 0; j < C::K4; ++j) Hb[row * C::PB + sg * C::K4 + j] = vout[j];
-                }
-            }
-            lds_barrier_abl<ABL>();
-            // ---- P5: y-window sums of Ha/Hb columns -> this slice's tile sums ---------------
-            {
-                const int col5 = tid % TX, seg5 = tid / TX;
-                const float* srca = Ha + (seg5 * K5) * C::PB + col5;
-                const float* srcb = Hb + (seg5 * K5) * C::PB + col5;
-                float vin[K5 + 2 * R];
-#pragma unroll
-                for (int j = 0; j < K5 + 2 * R; ++j) vin[j] = srca[j * C::PB];
-                tree_window_sums<R, K5>(vin, s2a);
-#pragma unroll
-                for (int j = 0; j < K5 + 2 * R; ++j) vin[j] = srcb[j * C::PB];
-                tree_window_sums<R, K5>(vin, s2b);
-            }
-        } else {
-#pragma unroll
-            for (int j = 0; j < K5; ++j) s2a[j] = s2b[j] = 0.0f;
+        for (int j = 0; j < C::K3; ++j) {
+            const int ey = sg * C::K3 + j, gy = y0 - R + ey;
+            const bool ok = xin && ey < C::E1Y && gy >= 0 && gy < ny;
+            v3[j] = (ABL & 2) ? 1.0f
+                              : Buf<TIn>::load(rc, ok ? (gy * sy + gx) * ESZ : kBadOff);
         }
-
-        // ---- ring: the z-window of the slice sums as an exact (f64) running sum, the ring
-        //      only supplies the value leaving the window. ----------------------------------
-        float olda[K5], oldb[K5];
-        // FIFO of the last W slice sums: read the leaving (oldest) entry, shift, append.
-        // A shift register keeps every index static (a runtime slot index would push the ring
-        // to scratch memory); it costs (W-1) moves per entry, no branches.
+    };
+    auto do_p3 = [&](int tid, int zc) {  // y-window (f64) of Hx -> U; a, b -> Lab
+        const int item = tid - C::T3;
+        if (item < 0) return;
+        const int col = item % C::E1X, sg = item / C::E1X;
+        const double* src = Hx + (sg * C::K3) * C::PH + col;
+        double vin[C::K3 + 2 * R], U[C::K3];
+#pragma unroll
+        for (int j = 0; j < C::K3 + 2 * R; ++j) vin[j] = src[j * C::PH];
+        slide_sums_f64<R, C::K3>(vin, U);
+        const int gx = x0 - R + col;
+        const bool xzin = gx >= 0 && gx < nx && zc >= 0 && zc < nz;
+        const int cxz = clamped_count(gx, nx, R) * clamped_count(zc, nz, R);
+#pragma unroll
+        for (int j = 0; j < C::K3; ++j) {
+            const int ey = sg * C::K3 + j;
+            const int gy = y0 - R + ey;
+            // summed_area_table_mean: (sum as f32) / (count as f32)
+            const int cnt = clamped_count(gy, ny, R) * cxz;
+            const float fc = (float)cnt;
+            const float rc = rcp_tab[cnt];
+            const float u = div_by_count((float)U[j], fc, rc);
+            const float d = v3[j] - u;
+            const float s = d * d;  // (v - u).powf(2.0)
+            float a, bb;
+            if constexpr (ABL & 32) {
+                a = s; bb = u;
+            } else {
+                a = fast_div(s, s + eps);
+                bb = (1.0f - a) * u;
+            }
+            const bool ok = xzin && gy >= 0 && gy < ny;  // zero outside: clamped window sums
+            if (ey < C::E1Y) Lab[ey * C::PA + col] = ok ? make_float2(a, bb) : make_float2(0.f, 0.f);
+        }
+    };
+    auto do_p4 = [&](int tid) {  // x-window sums of (a, b) rows -> Hab
+        const int item = tid;
+        if (item >= C::N4) return;
+        const int row = item % C::E1Y, sg = item / C::E1Y;
+        const float4* src = reinterpret_cast<const float4*>(Lab + row * C::PA + sg * C::K4);
+        float2 vin[C::K4 + 2 * R], vout[C::K4];
+#pragma unroll
+        for (int j = 0; j < (C::K4 + 2 * R) / 2; ++j) {
+            const float4 f = src[j];
+            vin[2 * j] = make_float2(f.x, f.y);
+            vin[2 * j + 1] = make_float2(f.z, f.w);
+        }
+        if constexpr ((C::K4 + 2 * R) % 2) vin[C::K4 + 2 * R - 1] = Lab[row * C::PA + sg * C::K4 + C::K4 + 2 * R - 1];
+        tree_window_sums_t<R, C::K4>(vin, vout);
+        float4* dst = reinterpret_cast<float4*>(Hab + row * C::PB + sg * C::K4);
+#pragma unroll
+        for (int j = 0; j < C::K4 / 2; ++j)
+            dst[j] = make_float4(vout[2 * j].x, vout[2 * j].y, vout[2 * j + 1].x, vout[2 * j + 1].y);
+    };
+    float v5[K5];  // v at this thread's outputs for the slice being emitted (prefetched)
+    auto load_v5 = [&](int tid, int zo) {
+        const int ox = x0 + tid % TX, oyb = y0 + (tid / TX) * K5;
+        const bool zok = zo >= zo_begin && zo < zo_end;
+        const rsrc_t rv = slice_rsrc(zok ? zo : -1);
 #pragma unroll
         for (int j = 0; j < K5; ++j) {
-            olda[j] = ring_a[0][j];
-            oldb[j] = ring_b[0][j];
-#pragma unroll
-            for (int t2 = 0; t2 + 1 < W; ++t2) {
-                ring_a[t2][j] = ring_a[t2 + 1][j];
-                ring_b[t2][j] = ring_b[t2 + 1][j];
-            }
-            ring_a[W - 1][j] = s2a[j];
-            ring_b[W - 1][j] = s2b[j];
+            const int oy = oyb + j;
+            const bool ok = ox < ox_end && oy < oy_end;
+            v5[j] = (ABL & 4) ? 1.0f
+                              : Buf<TIn>::load(rv, ok ? (oy * sy + ox) * ESZ : kBadOff);
         }
+    };
+    auto do_p5 = [&](int tid, int zc, auto slot_c) {  // y-window -> slice sums; ring; emit zc-R
+        const int col5 = tid % TX, seg5 = tid / TX;
+        const float2* src = Hab + (seg5 * K5) * C::PB + col5;
+        float2 vin[K5 + 2 * R], s2[K5];
+#pragma unroll
+        for (int j = 0; j < K5 + 2 * R; ++j) vin[j] = src[j * C::PB];
+        tree_window_sums_t<R, K5>(vin, s2);
+        // Ring of the last W slice sums, indexed by a compile-time slot (the march is unrolled
+        // by W, so every index is static and the ring stays in registers with no moves): the
+        // z-window is an exact f64 running sum, the ring supplies the leaving entry.
+        constexpr int SL = decltype(slot_c)::value;
         float A[K5], B[K5];
 #pragma unroll
         for (int j = 0; j < K5; ++j) {
-            za_run[j] = za_run[j] + (double)s2a[j];
-            za_run[j] = za_run[j] - (double)olda[j];
-            zb_run[j] = zb_run[j] + (double)s2b[j];
-            zb_run[j] = zb_run[j] - (double)oldb[j];
+            const float olda = ring_a[SL][j], oldb = ring_b[SL][j];
+            ring_a[SL][j] = s2[j].x;
+            ring_b[SL][j] = s2[j].y;
+            za_run[j] = za_run[j] + (double)s2[j].x;
+            za_run[j] = za_run[j] - (double)olda;
+            zb_run[j] = zb_run[j] + (double)s2[j].y;
+            zb_run[j] = zb_run[j] - (double)oldb;
             A[j] = (float)za_run[j];
             B[j] = (float)zb_run[j];
         }
-        if (emit) {
-            const int ox = x0 + tid % TX, oyb = y0 + (tid / TX) * K5;
+        const int zo = zc - R;
+        if (zo >= zo_begin) {
+            const int ox = x0 + col5, oyb = y0 + seg5 * K5;
             const int cxz = clamped_count(ox, nx, R) * clamped_count(zo, nz, R);
             const char* obase = static_cast<const char*>(p.out) +
                                 (int64_t)(zo - p.oz0) * p.out_sz * OSZ;
@@ -559,17 +581,53 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
                 const int oy = oyb + j;
                 const int cnt = clamped_count(oy, ny, R) * cxz;
                 const float fc = (float)cnt;
-                const float rc = cnt == C::W3 ? rcp_w3 : 1.0f / fc;
+                const float rc = rcp_tab[cnt];
                 const float ma = div_by_count(A[j], fc, rc);
                 const float mb = div_by_count(B[j], fc, rc);
                 const float o = __fadd_rn(__fmul_rn(v5[j], ma), mb);  // v *= ma; v += mb
                 const bool ok = ox < ox_end && oy < oy_end;
-                const int off =
-                    ok ? (int)(((int64_t)(oy - p.oy0) * p.out_sy + (ox - p.ox0)) * OSZ) : kBadOff;
+                const int off = ok ? ((oy - p.oy0) * osy + (ox - p.ox0)) * OSZ : kBadOff;
                 Buf<TOut>::store(from_f32<TOut>(o), ro, off);
             }
         }
+    };
+
+    // ---- prologue: stage 1 of the first slice up to Hx ------------------------------------
+    load_p1(zc_begin);
+    do_p1(tid0);
+    lds_barrier_abl<ABL>();
+    do_p2(tid0);
+    if (zc_begin + 1 < zc_end) load_p1(zc_begin + 1);
+    load_v3(tid0, zc_begin);
+    lds_barrier_abl<ABL>();
+
+    // ---- pipelined march, unrolled by W so the ring slot of every P5 is a constant ----------
+    for (int i0 = zc_begin; i0 < zc_end; i0 += W) {
+        static_for<0, W>([&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            const int i = i0 + k;
+            if (i >= zc_end) return;
+            const int tid = threadIdx.x;
+            const bool has_next = i + 1 < zc_end;
+            // C0: P3(i) + P1(i+1) + P5(i-1)
+            do_p3(tid, i);
+            if (has_next) do_p1(tid);
+            if (i > zc_begin) do_p5(tid, i - 1, std::integral_constant<int, (k + W - 1) % W>{});
+            // loads for the next iteration's C0 (latency hides under C1 and the barriers)
+            if (i + 2 < zc_end) load_p1(i + 2);
+            if (has_next) load_v3(tid, i + 1);
+            load_v5(tid, i - R);
+            lds_barrier_abl<ABL>();
+            // C1: P4(i) + P2(i+1)
+            do_p4(tid);
+            if (has_next) do_p2(tid);
+            lds_barrier_abl<ABL>();
+        });
     }
+    // ---- epilogue: stage 2 tail of the last slice (runtime slot -> dispatch, once) ----------
+    RingDispatch<0, W>::run((zc_end - 1 - zc_begin) % W, [&](auto slot_c) {
+        do_p5((int)threadIdx.x, zc_end - 1, slot_c);
+    });
 }
 
 // ---------------------------------------------------------------------------------------------
