@@ -226,13 +226,10 @@ using rsrc_t = __amdgpu_buffer_rsrc_t;
 constexpr int kBadOff = (int)0x80000000;  // >= num_records of any slice: reads 0, writes drop
 
 __device__ __forceinline__ rsrc_t make_rsrc(const void* base, uint32_t bytes) {
-    // Built from wave-uniform values only (T20): no waterfall loops around the buffer ops.
-    uint64_t b = (uint64_t)base;
-    uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
-    uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
-    bytes = __builtin_amdgcn_readfirstlane(bytes);
-    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0,
-                                             (int)bytes, 0x00020000);
+    // Callers build descriptors only from kernel arguments and loop counters (wave-uniform
+    // scalars), so hipcc keeps them in SGPRs: no readfirstlane, no waterfall loops (T20).
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes,
+                                             0x00020000);
 }
 
 template <typename T> struct Buf;
@@ -240,8 +237,10 @@ template <> struct Buf<float> {
     __device__ static float load(rsrc_t r, int off) {
         return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
     }
+    // Output stores are streamed with the non-temporal hint (aux 2 = nt) so they do not evict
+    // the input slices the march re-reads from L2 a few steps later.
     __device__ static void store(float v, rsrc_t r, int off) {
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, off, 0, 2);
     }
 };
 template <> struct Buf<uint16_t> {
@@ -249,7 +248,7 @@ template <> struct Buf<uint16_t> {
         return (float)(uint16_t)__builtin_amdgcn_raw_buffer_load_b16(r, off, 0, 0);
     }
     __device__ static void store(uint16_t v, rsrc_t r, int off) {
-        __builtin_amdgcn_raw_buffer_store_b16(v, r, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b16(v, r, off, 0, 2);
     }
 };
 template <> struct Buf<uint8_t> {
@@ -257,7 +256,7 @@ template <> struct Buf<uint8_t> {
         return (float)(uint8_t)__builtin_amdgcn_raw_buffer_load_b8(r, off, 0, 0);
     }
     __device__ static void store(uint8_t v, rsrc_t r, int off) {
-        __builtin_amdgcn_raw_buffer_store_b8(v, r, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b8(v, r, off, 0, 2);
     }
 };
 
