@@ -17,23 +17,12 @@ using namespace zt;
     printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
 
 template <int ABL>
-float run(const GFParams& p0, hipStream_t s, int reps) {
-    using C = GFConfig<4, 32, 1024>;
-    GFParams p = p0;
-    p.tiles_x = (p.onx + 63) / 64;
-    p.tiles_y = (p.ony + 31) / 32;
-    p.nseg = (p.onz + p.zseg - 1) / p.zseg;
-    p.rcp_w3 = 1.0f / 729.0f;
-    auto k = gf3d_fused_kernel<4, 32, 1024, float, float, ABL>;
-    CK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
-                           C::LDS_BYTES));
+float run(const GFParams& p, hipStream_t s, int reps) {
     hipEvent_t a, b;
     CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
-    int nwg = p.tiles_x * p.tiles_y * p.nseg;
-    hipLaunchKernelGGL(k, dim3(nwg), dim3(1024), C::LDS_BYTES, s, p);
+    CK((launch_fused_cfg<4, 32, 1024, float, float, ABL>(p, s)));
     CK(hipEventRecord(a, s));
-    for (int i = 0; i < reps; ++i)
-        hipLaunchKernelGGL(k, dim3(nwg), dim3(1024), C::LDS_BYTES, s, p);
+    for (int i = 0; i < reps; ++i) CK((launch_fused_cfg<4, 32, 1024, float, float, ABL>(p, s)));
     CK(hipEventRecord(b, s));
     CK(hipEventSynchronize(b));
     float ms; CK(hipEventElapsedTime(&ms, a, b));
@@ -54,24 +43,24 @@ int main(int argc, char** argv) {
     p.out_sy = n; p.in_z0 = 0; p.nz = p.ny = p.nx = n; p.oz0 = p.oy0 = p.ox0 = 0;
     p.onz = p.ony = p.onx = n; p.zseg = 256; p.eps = 2500.0f;
     hipStream_t s; CK(hipStreamCreate(&s));
-    const char* names[] = {"full", "no-leave-load(1)", "no-v3-load(2)", "no-v5-load(4)",
-                           "no-enter-load(8)", "no-barrier(16)", "no-pointwise(32)",
-                           "no-loads(15)", "no-loads+no-barrier(31)"};
-    std::vector<std::vector<float>> t(9);
+    const char* names[] = {"full", "no leave load (1)", "no Lc load (2)", "no v5 load (4)",
+                           "no enter load (8)", "no loads (15)", "no barrier (16)",
+                           "no pointwise (32)"};
+    constexpr int NV = 8;
+    std::vector<std::vector<float>> t(NV);
     for (int round = 0; round < 3; ++round) {
         t[0].push_back(run<0>(p, s, 3));
         t[1].push_back(run<1>(p, s, 3));
         t[2].push_back(run<2>(p, s, 3));
         t[3].push_back(run<4>(p, s, 3));
         t[4].push_back(run<8>(p, s, 3));
-        t[5].push_back(run<16>(p, s, 3));
-        t[6].push_back(run<32>(p, s, 3));
-        t[7].push_back(run<15>(p, s, 3));
-        t[8].push_back(run<31>(p, s, 3));
+        t[5].push_back(run<15>(p, s, 3));
+        t[6].push_back(run<16>(p, s, 3));
+        t[7].push_back(run<32>(p, s, 3));
     }
-    for (int i = 0; i < 9; ++i) {
+    for (int i = 0; i < NV; ++i) {
         std::sort(t[i].begin(), t[i].end());
-        printf("%-28s median %8.3f ms  min %8.3f ms  (%.1f GB/s algorithmic)\n", names[i],
+        printf("%-30s median %8.3f ms  min %8.3f ms  (%.1f GB/s algorithmic)\n", names[i],
                t[i][1], t[i][0], vox * 8.0 / (t[i][1] * 1e-3) / 1e9);
     }
     return 0;

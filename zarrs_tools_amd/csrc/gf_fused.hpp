@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <type_traits>
 
 #include "zt_device.hpp"
@@ -134,10 +135,57 @@ __device__ __forceinline__ void tree_window_sums_t(const T (&in)[K + 2 * R], T (
     }
 }
 
+
+// Packed pair of f32 (v_pk_add_f32 / v_pk_mul_f32 / v_pk_fma_f32: both lanes for one issue).
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+
+// Window sums of W = 2R+1 consecutive values for K consecutive outputs sharing one core:
+// every window contains in[K-1 .. W-1], so out_i = (in[i..K-2]) + core + (in[W..W+i-1]) with
+// the left parts built as suffix sums and the right parts as prefix sums: W + 3K - 6 adds
+// instead of a tree per output (9 vs 16 for K=2, 15 vs 26 for K=4 at R=4). Falls back to the
+// tree when K > W (tiny radii).
+template <int R, int K, typename T>
+__device__ __forceinline__ void core_window_sums(const T (&in)[K + 2 * R], T (&out)[K]);
+
 __device__ __forceinline__ int clamped_count(int i, int n, int r) {
     int lo = i - r < 0 ? 0 : i - r;
     int hi = i + r > n - 1 ? n - 1 : i + r;
     return hi - lo + 1;
+}
+
+template <int R, int K, typename T>
+__device__ __forceinline__ void core_window_sums(const T (&in)[K + 2 * R], T (&out)[K]) {
+    constexpr int W = 2 * R + 1;
+    if constexpr (K > W || K < 2) {
+        tree_window_sums_t<R, K>(in, out);
+    } else {
+        // core = in[K-1 .. W-1] summed pairwise (balanced)
+        constexpr int NC = W - K + 1;
+        T c[NC];
+#pragma unroll
+        for (int j = 0; j < NC; ++j) c[j] = in[K - 1 + j];
+#pragma unroll
+        for (int w = 1; w < NC; w *= 2) {
+#pragma unroll
+            for (int j = 0; j + w < NC; j += 2 * w) c[j] = c[j] + c[j + w];
+        }
+        const T core = c[0];
+        T left[K], right[K];  // left[i] = in[i..K-2], right[i] = in[W..W+i-1]
+        if constexpr (K >= 2) {
+            left[K - 2] = in[K - 2];
+#pragma unroll
+            for (int i = K - 3; i >= 0; --i) left[i] = in[i] + left[i + 1];
+            right[1] = in[W];
+#pragma unroll
+            for (int i = 2; i < K; ++i) right[i] = right[i - 1] + in[W + i - 1];
+        }
+        out[0] = left[0] + core;
+#pragma unroll
+        for (int i = 1; i < K - 1; ++i) out[i] = (left[i] + core) + right[i];
+        out[K - 1] = core + right[K - 1];
+    }
 }
 
 // Compile-time loop: f(integral_constant<I>) for I in [B, E).
@@ -260,16 +308,77 @@ template <> struct Buf<uint8_t> {
     }
 };
 
+// ---- 4 consecutive elements (one 16/8/4-byte buffer access per lane) ----------------------
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+template <typename T> struct Quad;
+template <> struct Quad<float> {
+    __device__ static void load(rsrc_t r, int off, float (&v)[4]) {
+        const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+        // (not __builtin_bit_cast on q.y: clang reads element 0 for a bit_cast of a vector
+        //  element lvalue)
+        v[0] = __uint_as_float(q.x); v[1] = __uint_as_float(q.y);
+        v[2] = __uint_as_float(q.z); v[3] = __uint_as_float(q.w);
+    }
+    __device__ static void store(const float (&v)[4], rsrc_t r, int off) {
+        const u32x4 q = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
+                         __float_as_uint(v[3])};
+        __builtin_amdgcn_raw_buffer_store_b128(q, r, off, 0, 2);
+    }
+};
+template <> struct Quad<uint16_t> {
+    __device__ static void load(rsrc_t r, int off, float (&v)[4]) {
+        const u32x2 q = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+        v[0] = (float)(q.x & 0xffffu); v[1] = (float)(q.x >> 16);
+        v[2] = (float)(q.y & 0xffffu); v[3] = (float)(q.y >> 16);
+    }
+    __device__ static void store(const float (&v)[4], rsrc_t r, int off) {
+        const uint32_t a = (uint32_t)from_f32<uint16_t>(v[0]) | ((uint32_t)from_f32<uint16_t>(v[1]) << 16);
+        const uint32_t b = (uint32_t)from_f32<uint16_t>(v[2]) | ((uint32_t)from_f32<uint16_t>(v[3]) << 16);
+        __builtin_amdgcn_raw_buffer_store_b64((u32x2){a, b}, r, off, 0, 2);
+    }
+};
+template <> struct Quad<uint8_t> {
+    __device__ static void load(rsrc_t r, int off, float (&v)[4]) {
+        const uint32_t q = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
+        v[0] = (float)(q & 0xffu); v[1] = (float)((q >> 8) & 0xffu);
+        v[2] = (float)((q >> 16) & 0xffu); v[3] = (float)(q >> 24);
+    }
+    __device__ static void store(const float (&v)[4], rsrc_t r, int off) {
+        const uint32_t a = (uint32_t)from_f32<uint8_t>(v[0]) | ((uint32_t)from_f32<uint8_t>(v[1]) << 8) |
+                           ((uint32_t)from_f32<uint8_t>(v[2]) << 16) | ((uint32_t)from_f32<uint8_t>(v[3]) << 24);
+        __builtin_amdgcn_raw_buffer_store_b32(a, r, off, 0, 2);
+    }
+};
+
+// A quad whose elements may lie partly outside the domain (edge tiles): element e is read at
+// off + e*size when bit e of mask is set, else reads 0 (kBadOff). Interior tiles use Quad::load.
+template <typename T>
+__device__ __forceinline__ void load_quad_masked(rsrc_t r, int off, int mask, float (&v)[4]) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+        v[e] = Buf<T>::load(r, (mask >> e) & 1 ? off + e * (int)sizeof(T) : kBadOff);
+}
+template <typename T>
+__device__ __forceinline__ void store_quad_masked(const float (&v)[4], rsrc_t r, int off, int mask) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+        Buf<T>::store(from_f32<T>(v[e]), r, (mask >> e) & 1 ? off + e * (int)sizeof(T) : kBadOff);
+}
+
 // ---------------------------------------------------------------------------------------------
 // The fused kernel.
 //
 // Software-pipelined phases, two LDS barriers per z-step. Iteration `i` runs
 //   C0: P3(i)  [U -> a,b on the E1 apron]  +  P1(i+1) [z-window of v]  +  P5(i-1) [y-sums,
-//       z-ring, emit out(i-1-R)]
-//   C1: P4(i)  [x-sums of (a,b)]           +  P2(i+1) [x-sums of the v z-window]
-// with separate LDS buffers per hand-off (Lv, Hx, Lab, Hab), so each barrier interval holds
-// independent work from different slices (better wave balance, half the barriers of a
-// straight P1..P5 sequence).
+//       z-blocks, out(i-1-R) -> Lout]
+//   C1: P4(i)  [x-sums of (a,b)]  +  P2(i+1) [x-sums of the v z-window]  +  staging: Lout ->
+//       global (16-B stores), v of slice i+1 -> Lc (P3's input), v of slice i-R -> Lv5 (P5's)
+// with separate LDS buffers per hand-off, so each barrier interval holds independent work from
+// different slices. Every global access is a 16-byte-per-lane quad (4 consecutive x) in
+// interior tiles: the kernel is bound by vector-memory instruction issue otherwise (one dword
+// per lane cost about as much as the whole pointwise stage).
 // ---------------------------------------------------------------------------------------------
 template <int R, int TY, int NT>
 struct GFConfig {
@@ -290,18 +399,27 @@ struct GFConfig {
     static constexpr int S3 = (E1Y + K3 - 1) / K3;   // segments per column, P3
     static constexpr int S4 = TX / K4;               // segments per row, P4
     static constexpr int N2 = E2Y * S2, N3 = E1X * S3, N4 = E1Y * S4;  // work items
-    static constexpr int R1 = NT / E2X;              // P1: apron rows per pass
-    static constexpr int NP1 = (E2Y + R1 - 1) / R1;  // P1: passes (positions per thread)
-    static constexpr int W3 = W * W * W;             // interior window count
+    // quads (4 consecutive x) of the global accesses
+    static constexpr int NQ1X = E2X / 4, NQ1 = NQ1X * E2Y;   // P1: the E2 apron
+    static constexpr int NQP1 = (NQ1 + NT - 1) / NT;         // P1 quads per thread
+    static constexpr int XC = R % 4;  // Lc quad grid starts XC elements left of the E1 apron
+    static constexpr int NQCX = (E1X + XC + 3) / 4, NQC = NQCX * E1Y;  // Lc: the E1 apron
+    static constexpr int PC = 4 * NQCX;                      // Lc pitch (floats)
+    static constexpr int NQ5 = TX / 4 * TY;                  // v5 / output tile quads
+    static constexpr int W3 = W * W * W;                     // interior window count
     static constexpr int al(int b) { return (b + 255) / 256 * 256; }
     static constexpr int SZ_LV = al((E2Y + 1) * PV * 8);
     static constexpr int SZ_HX = al((E2Y + K3) * PH * 8);
     static constexpr int SZ_LAB = al((E1Y + 1) * PA * 8);
     static constexpr int SZ_HAB = al((E1Y + 1) * PB * 8);
+    static constexpr int SZ_LC = al(E1Y * PC * 4);
+    static constexpr int SZ_T = al(TY * TX * 4);
     static constexpr int OFF_HX = SZ_LV, OFF_LAB = OFF_HX + SZ_HX, OFF_HAB = OFF_LAB + SZ_LAB;
-    static constexpr int OFF_RCP = OFF_HAB + SZ_HAB;
+    static constexpr int OFF_LC = OFF_HAB + SZ_HAB, OFF_LV5 = OFF_LC + SZ_LC;
+    static constexpr int OFF_LOUT = OFF_LV5 + SZ_T, OFF_RCP = OFF_LOUT + SZ_T;
     static constexpr int SZ_RCP = al((W3 + 1) * 4);  // RN(1/c) for window counts c <= W^3
-    static constexpr int LDS_BYTES = OFF_RCP + SZ_RCP;
+    static constexpr int OFF_DUMMY = OFF_RCP + SZ_RCP;  // 16-B sink for inactive lanes' writes
+    static constexpr int LDS_BYTES = OFF_DUMMY + 256;
     // item -> thread placement: heavy phases on different waves (see C0 / C1)
     static constexpr int T3 = NT - N3;  // P3 items on the top threads
     static constexpr int T2 = NT - N2;  // P2 items on the top threads, P4 on the bottom
@@ -309,11 +427,19 @@ struct GFConfig {
     static_assert(TY % K5 == 0, "ring segment must divide the tile height");
     static_assert(TX % K4 == 0, "P4 segment must divide the tile width");
     static_assert(N2 <= NT && N3 <= NT && N4 <= NT, "one work item per thread per phase");
-    static_assert(R1 >= 1, "P1 needs a full apron row per pass");
+    static_assert(NQC <= NT && NQ5 <= NT, "one staging quad per thread");
+    static_assert(E2X % 4 == 0, "E2 rows are whole quads");
     static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 };
 
-template <int R, int TY, int NT, typename TIn, typename TOut, int ABL = 0>
+// EDGE = false: the tiles [itx0, itx1) x [ity0, ity1), where every 4-element quad of a global
+// access is either entirely inside the domain / output box or entirely outside (all tiles when
+// the geometry is quad-aligned, else the interior tiles): unmasked 16-byte accesses, the
+// outside quads through kBadOff. EDGE = true: every other tile (the grid covers all tiles;
+// those of the first launch return at once), element-wise masked accesses. Two kernels rather
+// than a runtime branch keep each march free of control flow around its memory instructions,
+// so the compiler's vmcnt accounting stays exact (a branch there made it drain every load).
+template <int R, int TY, int NT, typename TIn, typename TOut, bool EDGE, int ABL = 0>
 __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     using C = GFConfig<R, TY, NT>;
     constexpr int TX = C::TX, W = C::W;
@@ -324,6 +450,9 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     double* Hx = reinterpret_cast<double*>(smem + C::OFF_HX);
     float2* Lab = reinterpret_cast<float2*>(smem + C::OFF_LAB);
     float2* Hab = reinterpret_cast<float2*>(smem + C::OFF_HAB);
+    float* Lc = reinterpret_cast<float*>(smem + C::OFF_LC);
+    float* Lv5 = reinterpret_cast<float*>(smem + C::OFF_LV5);
+    float* Lout = reinterpret_cast<float*>(smem + C::OFF_LOUT);
     float* rcp_tab = reinterpret_cast<float*>(smem + C::OFF_RCP);
     // Correctly rounded reciprocals of every possible window count, for div_by_count
     // (Markstein's correction needs RN(1/c) exactly). Published by the prologue's barriers.
@@ -335,30 +464,38 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     const int nwg = gridDim.x;
     const int b = blockIdx.x;
     const int lid = (nwg % 8 == 0) ? (b % 8) * (nwg / 8) + b / 8 : b;
-    const int ntiles = p.tiles_x * p.tiles_y;
+    const int gtx = EDGE ? p.tiles_x : p.itx1 - p.itx0;  // this launch's tile grid
+    const int gty = EDGE ? p.tiles_y : p.ity1 - p.ity0;
+    const int ntiles = gtx * gty;
     const int seg = lid / ntiles;
     int t = lid % ntiles;
     int tile_x, tile_y;
     {
         const int stx = 8, sty = 4;
-        const int full_y = p.tiles_y / sty * sty;
-        const int per_srow = p.tiles_x * sty;
-        if (t < full_y * p.tiles_x) {
+        const int full_y = gty / sty * sty;
+        const int per_srow = gtx * sty;
+        if (t < full_y * gtx) {
             const int sr = t / per_srow, r = t % per_srow;
-            const int full_x = p.tiles_x / stx * stx;
+            const int full_x = gtx / stx * stx;
             if (r < full_x * sty) {
                 tile_x = (r / (stx * sty)) * stx + r % stx;
                 tile_y = sr * sty + (r / stx) % sty;
             } else {
-                const int rr = r - full_x * sty, w = p.tiles_x - full_x;
+                const int rr = r - full_x * sty, w = gtx - full_x;
                 tile_x = full_x + rr % w;
                 tile_y = sr * sty + rr / w;
             }
         } else {
-            t -= full_y * p.tiles_x;
-            tile_x = t % p.tiles_x;
-            tile_y = full_y + t / p.tiles_x;
+            t -= full_y * gtx;
+            tile_x = t % gtx;
+            tile_y = full_y + t / gtx;
         }
+    }
+    if constexpr (EDGE) {
+        if (tile_x >= p.itx0 && tile_x < p.itx1 && tile_y >= p.ity0 && tile_y < p.ity1) return;
+    } else {
+        tile_x += p.itx0;
+        tile_y += p.ity0;
     }
 
     const int x0 = p.ox0 + tile_x * TX;
@@ -380,26 +517,68 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
         return make_rsrc(base, ok ? slice_bytes : 0u);
     };
 
-    // ---- per-thread, step-invariant byte offsets (kBadOff where outside the domain) --------
-    const int tid0 = threadIdx.x;
-    int p1off[C::NP1];
-    {
-        const int row0 = tid0 / C::E2X, col = tid0 % C::E2X;
-        const int gx = x0 - 2 * R + col;
-        const bool xin = tid0 < C::R1 * C::E2X && gx >= 0 && gx < nx;
-#pragma unroll
-        for (int k = 0; k < C::NP1; ++k) {
-            const int row = row0 + k * C::R1;
-            const int gy = y0 - 2 * R + row;
-            const bool ok = xin && row < C::E2Y && gy >= 0 && gy < ny;
-            p1off[k] = ok ? (gy * sy + gx) * ESZ : kBadOff;
-        }
-    }
-
-    double zv[C::NP1];
-#pragma unroll
-    for (int k = 0; k < C::NP1; ++k) zv[k] = 0.0;
     const int zc_begin = zo_begin - R, zc_end = zo_end + R;  // stage-1 slices of this march
+    // Interior tiles (see launch_fused_cfg): window counts are W^3 wherever z is interior too,
+    // so P3/P5 take a branch-free path with the constant correctly rounded 1/W^3
+    // (host-computed).
+    const bool xy_interior = x0 - 2 * R >= 0 && x0 + TX + 2 * R <= nx && y0 - 2 * R >= 0 &&
+                             y0 + TY + 2 * R <= ny;  // wave-uniform
+    constexpr float kW3 = (float)C::W3;
+    const float rcp_w3 = p.rcp_w3;
+
+    // ---- per-thread, step-invariant quad offsets and in-domain masks -----------------------
+    const int tid0 = threadIdx.x;
+    int q1off[C::NQP1], q1mask[C::NQP1];
+#pragma unroll
+    for (int k = 0; k < C::NQP1; ++k) {
+        const int q = tid0 + k * NT;
+        const int row = q / C::NQ1X, cq = q % C::NQ1X;
+        const int gx = x0 - 2 * R + 4 * cq, gy = y0 - 2 * R + row;
+        int m = 0;
+        if (q < C::NQ1 && gy >= 0 && gy < ny) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) m |= (gx + e >= 0 && gx + e < nx) ? (1 << e) : 0;
+        }
+        q1mask[k] = m;
+        q1off[k] = (EDGE ? q < C::NQ1 : m == 0xF) ? (gy * sy + gx) * ESZ : kBadOff;
+    }
+    // Lc / v5 / output quads: offsets and masks are recomputed at their one use per step
+    // (a few integer ops) rather than held in registers across the march.
+    // P3's center slice on the E1 apron, on the quad grid of E2 (first quad starts C::XC
+    // elements left of the E1 apron), so Lc quads are aligned like P1's
+    auto quad_c = [&](int tid, int& off, int& mask) {
+        const int row = tid / C::NQCX, cq = tid % C::NQCX;
+        const int gx = x0 - R - C::XC + 4 * cq, gy = y0 - R + row;
+        int m = 0;
+        if (tid < C::NQC && gy >= 0 && gy < ny) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) m |= (gx + e >= 0 && gx + e < nx) ? (1 << e) : 0;
+        }
+        mask = m;
+        off = (EDGE ? tid < C::NQC : m == 0xF) ? (gy * sy + gx) * ESZ : kBadOff;
+    };
+    auto quad_t = [&](int q, int& ox, int& oy, int& mask) {  // tile quad q: output positions
+        const int row = q / (TX / 4), cq = q % (TX / 4);
+        ox = x0 + 4 * cq;
+        oy = y0 + row;
+        int m = 0;
+        if (q >= 0 && q < C::NQ5 && oy < oy_end) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) m |= (ox + e < ox_end) ? (1 << e) : 0;
+        }
+        mask = m;
+    };
+
+    auto load_quad = [&](rsrc_t r, int off, int mask, float (&v)[4]) {
+        if constexpr (EDGE) load_quad_masked<TIn>(r, off, mask, v);
+        else Quad<TIn>::load(r, off, v);
+    };
+
+    double zv[C::NQP1][4];
+#pragma unroll
+    for (int k = 0; k < C::NQP1; ++k)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) zv[k][e] = 0.0;
     // Running z-window: seed Zv(zc_begin - 1) = sum of v over [zc_begin-1-R, zc_begin-1+R]
     // clamped to [0, nz); every later step adds the entering and subtracts the leaving slice
     // (both 0 outside the domain), so the window stays exact through out-of-domain steps.
@@ -408,39 +587,49 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
         for (int z = zlo; z <= zhi; ++z) {
             const rsrc_t rs = slice_rsrc(z);
 #pragma unroll
-            for (int k = 0; k < C::NP1; ++k) zv[k] += (double)Buf<TIn>::load(rs, p1off[k]);
+            for (int k = 0; k < C::NQP1; ++k) {
+                float v[4];
+                load_quad(rs, q1off[k], q1mask[k], v);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) zv[k][e] += (double)v[e];
+            }
         }
     }
 
-    float ring_a[W][K5], ring_b[W][K5];
+    f2 ring[W][K5], pre[K5];  // stage-2 z blocks (see do_p5)
 #pragma unroll
     for (int s = 0; s < W; ++s)
 #pragma unroll
-        for (int j = 0; j < K5; ++j) ring_a[s][j] = ring_b[s][j] = 0.0f;
-    double za_run[K5], zb_run[K5];
+        for (int j = 0; j < K5; ++j) ring[s][j] = (f2){0.0f, 0.0f};
 #pragma unroll
-    for (int j = 0; j < K5; ++j) za_run[j] = zb_run[j] = 0.0;
+    for (int j = 0; j < K5; ++j) pre[j] = (f2){0.0f, 0.0f};
 
     // ---- phase bodies ----------------------------------------------------------------------
-    float pa[C::NP1], ps[C::NP1];  // P1 inputs for the next stage-1 slice (prefetched)
-    auto load_p1 = [&](int zc) {    // entering slice zc+R and leaving slice zc-R-1 of step zc
-        const rsrc_t ra = slice_rsrc(zc + R);
-        const rsrc_t rs = slice_rsrc(zc - R - 1);
+    float pa[C::NQP1][4], ps[C::NQP1][4];  // P1 inputs for the next stage-1 slice (prefetched)
+    auto load_p1 = [&](rsrc_t ra, rsrc_t rs) {  // entering slice zc+R, leaving slice zc-R-1
 #pragma unroll
-        for (int k = 0; k < C::NP1; ++k) {
-            pa[k] = (ABL & 8) ? 1.0f : Buf<TIn>::load(ra, p1off[k]);
-            ps[k] = (ABL & 1) ? 0.5f : Buf<TIn>::load(rs, p1off[k]);
+        for (int k = 0; k < C::NQP1; ++k) {
+            if constexpr (ABL & 8) { for (int e = 0; e < 4; ++e) pa[k][e] = 1.0f; }
+            else load_quad(ra, q1off[k], q1mask[k], pa[k]);
+            if constexpr (ABL & 1) { for (int e = 0; e < 4; ++e) ps[k][e] = 0.5f; }
+            else load_quad(rs, q1off[k], q1mask[k], ps[k]);
         }
     };
     auto do_p1 = [&](int tid) {  // z-window of v (f64) on the E2 apron -> Lv
-        const int row0 = tid / C::E2X, col = tid % C::E2X;
-        double* dst = Lv + row0 * C::PV + col;
-        const bool act = tid < C::R1 * C::E2X;
 #pragma unroll
-        for (int k = 0; k < C::NP1; ++k) {
-            zv[k] = zv[k] + (double)pa[k];  // entering slice zc+R (0 outside the domain)
-            zv[k] = zv[k] - (double)ps[k];  // leaving slice zc-R-1 (0 outside the domain)
-            if (act && row0 + k * C::R1 < C::E2Y) dst[k * C::R1 * C::PV] = zv[k];
+        for (int k = 0; k < C::NQP1; ++k) {
+            const int q = tid + k * NT;
+            const int row = q / C::NQ1X, cq = q % C::NQ1X;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                zv[k][e] = zv[k][e] + (double)pa[k][e];  // entering slice (0 outside the domain)
+                zv[k][e] = zv[k][e] - (double)ps[k][e];  // leaving slice (0 outside the domain)
+            }
+            if (q < C::NQ1) {
+                double2* dst = reinterpret_cast<double2*>(Lv + row * C::PV + 4 * cq);
+                dst[0] = make_double2(zv[k][0], zv[k][1]);
+                dst[1] = make_double2(zv[k][2], zv[k][3]);
+            }
         }
     };
     auto do_p2 = [&](int tid) {  // x-window sums (f64) of Lv rows -> Hx
@@ -463,21 +652,51 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
         for (int j = 0; j < C::K2 / 2; ++j)
             if (sg * C::K2 + 2 * j < C::E1X) dst[j] = make_double2(vout[2 * j], vout[2 * j + 1]);
     };
-    float v3[C::K3];  // v at the P3 item's E1 positions, slice i (prefetched one step ahead)
-    auto load_v3 = [&](int tid, int zc) {
-        const int item = tid - C::T3;
-        const int col = item % C::E1X, sg = item / C::E1X;
-        const int gx = x0 - R + col;
-        const bool xin = item >= 0 && gx >= 0 && gx < nx;
-        const rsrc_t rc = slice_rsrc(zc);
+    // Pointwise stage on NP pairs of E1 positions, packed (both lanes of every op in one issue)
+    // and written op-by-op across the pairs so dependent packed ops are interleaved (gfx950
+    // needs an s_nop between back-to-back dependent v_pk_* otherwise):
+    //   u = RN(RN(U) / c)   (summed_area_table_mean, exact: Markstein with rcp = RN(1/c))
+    //   s = (v - u)^2;  a = s / (s + eps);  b = (1 - a) * u          (guided_filter.rs:126-137)
+    constexpr int NP3 = C::K3 / 2;
+    auto pointwise = [&](const f2 (&Uf)[NP3], const f2 (&v)[NP3], const f2 (&fc)[NP3],
+                         const f2 (&rc)[NP3], f2 (&a)[NP3], f2 (&bb)[NP3]) {
+        f2 q[NP3], r[NP3], u[NP3], sq[NP3], den[NP3], y[NP3], e[NP3];
 #pragma unroll
-        for (int j = 0; j < C::K3; ++j) {
-            const int ey = sg * C::K3 + j, gy = y0 - R + ey;
-            const bool ok = xin && ey < C::E1Y && gy >= 0 && gy < ny;
-            v3[j] = (ABL & 2) ? 1.0f
-                              : Buf<TIn>::load(rc, ok ? (gy * sy + gx) * ESZ : kBadOff);
+        for (int k = 0; k < NP3; ++k) q[k] = Uf[k] * rc[k];
+#pragma unroll
+        for (int k = 0; k < NP3; ++k) r[k] = pk_fma(-q[k], fc[k], Uf[k]);
+#pragma unroll
+        for (int k = 0; k < NP3; ++k) u[k] = pk_fma(r[k], rc[k], q[k]);
+#pragma unroll
+        for (int k = 0; k < NP3; ++k) sq[k] = v[k] - u[k];
+#pragma unroll
+        for (int k = 0; k < NP3; ++k) sq[k] = sq[k] * sq[k];  // (v - u).powf(2.0)
+        if constexpr (ABL & 32) {
+#pragma unroll
+            for (int k = 0; k < NP3; ++k) { a[k] = sq[k]; bb[k] = u[k]; }
+        } else {
+#pragma unroll
+            for (int k = 0; k < NP3; ++k) den[k] = sq[k] + (f2){eps, eps};
+#pragma unroll
+            for (int k = 0; k < NP3; ++k)
+                y[k] = (f2){__builtin_amdgcn_rcpf(den[k].x), __builtin_amdgcn_rcpf(den[k].y)};
+#pragma unroll
+            for (int k = 0; k < NP3; ++k) e[k] = pk_fma(-den[k], y[k], (f2){1.0f, 1.0f});
+#pragma unroll
+            for (int k = 0; k < NP3; ++k) y[k] = pk_fma(e[k], y[k], y[k]);
+#pragma unroll
+            for (int k = 0; k < NP3; ++k) q[k] = sq[k] * y[k];
+#pragma unroll
+            for (int k = 0; k < NP3; ++k) r[k] = pk_fma(-den[k], q[k], sq[k]);
+#pragma unroll
+            for (int k = 0; k < NP3; ++k) a[k] = pk_fma(r[k], y[k], q[k]);
+#pragma unroll
+            for (int k = 0; k < NP3; ++k) e[k] = (f2){1.0f, 1.0f} - a[k];
+#pragma unroll
+            for (int k = 0; k < NP3; ++k) bb[k] = e[k] * u[k];
         }
     };
+    static_assert(C::K3 % 2 == 0, "P3 works on pairs");
     auto do_p3 = [&](int tid, int zc) {  // y-window (f64) of Hx -> U; a, b -> Lab
         const int item = tid - C::T3;
         if (item < 0) return;
@@ -487,29 +706,49 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
 #pragma unroll
         for (int j = 0; j < C::K3 + 2 * R; ++j) vin[j] = src[j * C::PH];
         slide_sums_f64<R, C::K3>(vin, U);
+        const float* vsrc = Lc + (sg * C::K3) * C::PC + C::XC + col;  // v of slice zc (C1)
+        f2* lab = reinterpret_cast<f2*>(Lab);
+        f2 Uf[NP3], vv[NP3], fc[NP3], rc[NP3], a[NP3], bb[NP3];
+#pragma unroll
+        for (int k = 0; k < NP3; ++k) {
+            Uf[k] = (f2){(float)U[2 * k], (float)U[2 * k + 1]};
+            vv[k] = (f2){vsrc[(2 * k) * C::PC], vsrc[(2 * k + 1) * C::PC]};
+        }
+        if (xy_interior && zc - R >= 0 && zc + R < nz) {  // wave-uniform: count = W^3
+#pragma unroll
+            for (int k = 0; k < NP3; ++k) {
+                fc[k] = (f2){kW3, kW3};
+                rc[k] = (f2){rcp_w3, rcp_w3};
+            }
+            pointwise(Uf, vv, fc, rc, a, bb);
+#pragma unroll
+            for (int k = 0; k < NP3; ++k) {
+                const int ey = sg * C::K3 + 2 * k;
+                if (ey < C::E1Y) lab[ey * C::PA + col] = (f2){a[k].x, bb[k].x};
+                if (ey + 1 < C::E1Y) lab[(ey + 1) * C::PA + col] = (f2){a[k].y, bb[k].y};
+            }
+            return;
+        }
         const int gx = x0 - R + col;
         const bool xzin = gx >= 0 && gx < nx && zc >= 0 && zc < nz;
         const int cxz = clamped_count(gx, nx, R) * clamped_count(zc, nz, R);
 #pragma unroll
-        for (int j = 0; j < C::K3; ++j) {
-            const int ey = sg * C::K3 + j;
+        for (int k = 0; k < NP3; ++k) {
+            const int gy = y0 - R + sg * C::K3 + 2 * k;
+            const int c0 = clamped_count(gy, ny, R) * cxz, c1 = clamped_count(gy + 1, ny, R) * cxz;
+            fc[k] = (f2){(float)c0, (float)c1};
+            rc[k] = (f2){rcp_tab[c0], rcp_tab[c1]};
+        }
+        pointwise(Uf, vv, fc, rc, a, bb);
+#pragma unroll
+        for (int k = 0; k < NP3; ++k) {
+            const int ey = sg * C::K3 + 2 * k;
             const int gy = y0 - R + ey;
-            // summed_area_table_mean: (sum as f32) / (count as f32)
-            const int cnt = clamped_count(gy, ny, R) * cxz;
-            const float fc = (float)cnt;
-            const float rc = rcp_tab[cnt];
-            const float u = div_by_count((float)U[j], fc, rc);
-            const float d = v3[j] - u;
-            const float s = d * d;  // (v - u).powf(2.0)
-            float a, bb;
-            if constexpr (ABL & 32) {
-                a = s; bb = u;
-            } else {
-                a = fast_div(s, s + eps);
-                bb = (1.0f - a) * u;
-            }
-            const bool ok = xzin && gy >= 0 && gy < ny;  // zero outside: clamped window sums
-            if (ey < C::E1Y) Lab[ey * C::PA + col] = ok ? make_float2(a, bb) : make_float2(0.f, 0.f);
+            // zero outside the domain: the clamped window sums of stage 2
+            const bool ok0 = xzin && gy >= 0 && gy < ny, ok1 = xzin && gy + 1 >= 0 && gy + 1 < ny;
+            if (ey < C::E1Y) lab[ey * C::PA + col] = ok0 ? (f2){a[k].x, bb[k].x} : (f2){0.f, 0.f};
+            if (ey + 1 < C::E1Y)
+                lab[(ey + 1) * C::PA + col] = ok1 ? (f2){a[k].y, bb[k].y} : (f2){0.f, 0.f};
         }
     };
     auto do_p4 = [&](int tid) {  // x-window sums of (a, b) rows -> Hab
@@ -517,122 +756,237 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
         if (item >= C::N4) return;
         const int row = item % C::E1Y, sg = item / C::E1Y;
         const float4* src = reinterpret_cast<const float4*>(Lab + row * C::PA + sg * C::K4);
-        float2 vin[C::K4 + 2 * R], vout[C::K4];
+        f2 vin[C::K4 + 2 * R], vout[C::K4];
 #pragma unroll
         for (int j = 0; j < (C::K4 + 2 * R) / 2; ++j) {
             const float4 f = src[j];
-            vin[2 * j] = make_float2(f.x, f.y);
-            vin[2 * j + 1] = make_float2(f.z, f.w);
+            vin[2 * j] = (f2){f.x, f.y};
+            vin[2 * j + 1] = (f2){f.z, f.w};
         }
-        if constexpr ((C::K4 + 2 * R) % 2) vin[C::K4 + 2 * R - 1] = Lab[row * C::PA + sg * C::K4 + C::K4 + 2 * R - 1];
-        tree_window_sums_t<R, C::K4>(vin, vout);
+        if constexpr ((C::K4 + 2 * R) % 2) {
+            const float2 t = Lab[row * C::PA + sg * C::K4 + C::K4 + 2 * R - 1];
+            vin[C::K4 + 2 * R - 1] = (f2){t.x, t.y};
+        }
+        core_window_sums<R, C::K4>(vin, vout);
         float4* dst = reinterpret_cast<float4*>(Hab + row * C::PB + sg * C::K4);
 #pragma unroll
         for (int j = 0; j < C::K4 / 2; ++j)
             dst[j] = make_float4(vout[2 * j].x, vout[2 * j].y, vout[2 * j + 1].x, vout[2 * j + 1].y);
     };
-    float v5[K5];  // v at this thread's outputs for the slice being emitted (prefetched)
-    auto load_v5 = [&](int tid, int zo) {
-        const int ox = x0 + tid % TX, oyb = y0 + (tid / TX) * K5;
-        const bool zok = zo >= zo_begin && zo < zo_end;
-        const rsrc_t rv = slice_rsrc(zok ? zo : -1);
-#pragma unroll
-        for (int j = 0; j < K5; ++j) {
-            const int oy = oyb + j;
-            const bool ok = ox < ox_end && oy < oy_end;
-            v5[j] = (ABL & 4) ? 1.0f
-                              : Buf<TIn>::load(rv, ok ? (oy * sy + ox) * ESZ : kBadOff);
-        }
-    };
-    auto do_p5 = [&](int tid, int zc, auto slot_c) {  // y-window -> slice sums; ring; emit zc-R
+    // Stage-2 z-window by prefix/suffix sums over blocks of W slices (van Herk / Gil-Werman):
+    // the march is unrolled by W, so the position P of a slice in its block is a compile-time
+    // constant. ring[P] holds the raw slice sum of the current block until the block's last
+    // slice, when it is turned into the suffix sum over [P, W) in place; a window ending at
+    // position P of block B+1 is suffix_B(P+1) + prefix_{B+1}(P). ~3 packed adds per output
+    // instead of an f64 running sum (10 ops).
+    auto do_p5 = [&](int tid, int zc, auto slot_c) {  // y-window -> slice sums; z; out -> Lout
         const int col5 = tid % TX, seg5 = tid / TX;
-        const float2* src = Hab + (seg5 * K5) * C::PB + col5;
-        float2 vin[K5 + 2 * R], s2[K5];
+        const f2* src = reinterpret_cast<const f2*>(Hab) + (seg5 * K5) * C::PB + col5;
+        f2 vin[K5 + 2 * R], s2[K5];
 #pragma unroll
         for (int j = 0; j < K5 + 2 * R; ++j) vin[j] = src[j * C::PB];
-        tree_window_sums_t<R, K5>(vin, s2);
-        // Ring of the last W slice sums, indexed by a compile-time slot (the march is unrolled
-        // by W, so every index is static and the ring stays in registers with no moves): the
-        // z-window is an exact f64 running sum, the ring supplies the leaving entry.
-        constexpr int SL = decltype(slot_c)::value;
-        float A[K5], B[K5];
+        core_window_sums<R, K5>(vin, s2);
+        constexpr int P = decltype(slot_c)::value;
+        f2 AB[K5];
 #pragma unroll
         for (int j = 0; j < K5; ++j) {
-            const float olda = ring_a[SL][j], oldb = ring_b[SL][j];
-            ring_a[SL][j] = s2[j].x;
-            ring_b[SL][j] = s2[j].y;
-            za_run[j] = za_run[j] + (double)s2[j].x;
-            za_run[j] = za_run[j] - (double)olda;
-            zb_run[j] = zb_run[j] + (double)s2[j].y;
-            zb_run[j] = zb_run[j] - (double)oldb;
-            A[j] = (float)za_run[j];
-            B[j] = (float)zb_run[j];
+            pre[j] = (P == 0) ? s2[j] : pre[j] + s2[j];
+            if constexpr (P == W - 1) AB[j] = pre[j];
+            else AB[j] = ring[(P + 1) % W][j] + pre[j];
+            ring[P][j] = s2[j];
+        }
+        if constexpr (P == W - 1) {
+#pragma unroll
+            for (int q = W - 2; q >= 0; --q)
+#pragma unroll
+                for (int j = 0; j < K5; ++j) ring[q][j] = ring[q][j] + ring[q + 1][j];
         }
         const int zo = zc - R;
-        if (zo >= zo_begin) {
-            const int ox = x0 + col5, oyb = y0 + seg5 * K5;
-            const int cxz = clamped_count(ox, nx, R) * clamped_count(zo, nz, R);
-            const char* obase = static_cast<const char*>(p.out) +
-                                (int64_t)(zo - p.oz0) * p.out_sz * OSZ;
-            const rsrc_t ro = make_rsrc(obase, oslice_bytes);
+        if (zo < zo_begin || zo >= zo_end) return;  // wave-uniform
+        const int ox = x0 + col5, oyb = y0 + seg5 * K5;
+        const bool interior = xy_interior && zo - R >= 0 && zo + R < nz;  // wave-uniform
+        const int cxz = interior ? 0 : clamped_count(ox, nx, R) * clamped_count(zo, nz, R);
+        f2 fc[K5], rc[K5], q[K5], r[K5];
 #pragma unroll
-            for (int j = 0; j < K5; ++j) {
-                const int oy = oyb + j;
-                const int cnt = clamped_count(oy, ny, R) * cxz;
-                const float fc = (float)cnt;
-                const float rc = rcp_tab[cnt];
-                const float ma = div_by_count(A[j], fc, rc);
-                const float mb = div_by_count(B[j], fc, rc);
-                const float o = __fadd_rn(__fmul_rn(v5[j], ma), mb);  // v *= ma; v += mb
-                const bool ok = ox < ox_end && oy < oy_end;
-                const int off = ok ? ((oy - p.oy0) * osy + (ox - p.ox0)) * OSZ : kBadOff;
-                Buf<TOut>::store(from_f32<TOut>(o), ro, off);
+        for (int j = 0; j < K5; ++j) {
+            if (interior) {
+                fc[j] = (f2){kW3, kW3};
+                rc[j] = (f2){rcp_w3, rcp_w3};
+            } else {
+                const int cnt = clamped_count(oyb + j, ny, R) * cxz;
+                const float f = (float)cnt, rr = rcp_tab[cnt];
+                fc[j] = (f2){f, f};
+                rc[j] = (f2){rr, rr};
             }
+        }
+        // (sum as f32) / (count as f32) for a and b together (exact: Markstein)
+#pragma unroll
+        for (int j = 0; j < K5; ++j) q[j] = AB[j] * rc[j];
+#pragma unroll
+        for (int j = 0; j < K5; ++j) r[j] = pk_fma(-q[j], fc[j], AB[j]);
+#pragma unroll
+        for (int j = 0; j < K5; ++j) q[j] = pk_fma(r[j], rc[j], q[j]);
+#pragma unroll
+        for (int j = 0; j < K5; ++j) {
+            const int ty = seg5 * K5 + j;
+            const float v = Lv5[ty * TX + col5];                  // v of slice zo (staged in C1)
+            Lout[ty * TX + col5] = __fadd_rn(__fmul_rn(v, q[j].x), q[j].y);  // v*=ma; v+=mb
         }
     };
 
-    // ---- prologue: stage 1 of the first slice up to Hx ------------------------------------
-    load_p1(zc_begin);
+    // ---- C1 staging: 16-byte quads between global memory and the LDS tiles ------------------
+    // Every global access of the march below is unconditional, in the same order every step:
+    // out-of-range slices, inactive lanes and non-emitting steps use null descriptors or
+    // kBadOff instead of branches. Branches around memory instructions make the compiler's
+    // vmcnt accounting fall back to draining the loads just issued (measured: a 1.6x slower
+    // kernel); straight-line, it waits for exactly the step-old load it needs.
+    float cq4[4], vq4[4];  // v of the next Lc slice / the next Lv5 slice (prefetched a step ahead)
+    auto load_c = [&](rsrc_t r) {
+        if constexpr (ABL & 2) { for (int e = 0; e < 4; ++e) cq4[e] = 1.0f; }
+        else {
+            int off, mask;
+            quad_c((int)threadIdx.x, off, mask);
+            load_quad(r, off, mask, cq4);
+        }
+    };
+    auto load_v5 = [&](rsrc_t r) {
+        if constexpr (ABL & 4) { for (int e = 0; e < 4; ++e) vq4[e] = 1.0f; }
+        else {
+            const int q = (int)threadIdx.x - (NT - C::NQ5);
+            int ox, oy, mask;
+            quad_t(q, ox, oy, mask);
+            const int off = (EDGE ? q >= 0 : mask == 0xF) ? (oy * sy + ox) * ESZ : kBadOff;
+            load_quad(r, off, mask, vq4);
+        }
+    };
+    float* const dummy = reinterpret_cast<float*>(smem + C::OFF_DUMMY);  // inactive lanes' writes
+    auto write_c = [&](int tid) {
+        const int row = tid / C::NQCX, cq = tid % C::NQCX;
+        float* dst = tid < C::NQC ? Lc + row * C::PC + 4 * cq : dummy;
+        *reinterpret_cast<float4*>(dst) = make_float4(cq4[0], cq4[1], cq4[2], cq4[3]);
+    };
+    auto write_v5 = [&](int tid) {
+        const int q = tid - (NT - C::NQ5);
+        const int row = q / (TX / 4), cq = q % (TX / 4);
+        float* dst = q >= 0 ? Lv5 + row * TX + 4 * cq : dummy;
+        *reinterpret_cast<float4*>(dst) = make_float4(vq4[0], vq4[1], vq4[2], vq4[3]);
+    };
+    auto store_out = [&](int tid, rsrc_t ro) {  // Lout -> global, one quad per thread
+        const bool act = tid < C::NQ5;
+        const int row = act ? tid / (TX / 4) : 0, cq = act ? tid % (TX / 4) : 0;
+        const float4 o4 = *reinterpret_cast<const float4*>(Lout + row * TX + 4 * cq);
+        const float o[4] = {o4.x, o4.y, o4.z, o4.w};
+        int ox, oy, mask;
+        quad_t(tid, ox, oy, mask);
+        const int off =
+            (EDGE ? act : mask == 0xF) ? ((oy - p.oy0) * osy + (ox - p.ox0)) * OSZ : kBadOff;
+        if constexpr (EDGE) store_quad_masked<TOut>(o, ro, off, mask);
+        else Quad<TOut>::store(o, ro, off);
+    };
+
+    // ---- prologue: stage 1 of the first slice up to Hx, first Lc ---------------------------
+    load_p1(slice_rsrc(zc_begin + R), slice_rsrc(zc_begin - R - 1));
+    load_c(slice_rsrc(zc_begin));
     do_p1(tid0);
+    write_c(tid0);
     lds_barrier_abl<ABL>();
     do_p2(tid0);
-    if (zc_begin + 1 < zc_end) load_p1(zc_begin + 1);
-    load_v3(tid0, zc_begin);
+    load_p1(slice_rsrc(zc_begin + 1 + R), slice_rsrc(zc_begin - R));
+    load_c(slice_rsrc(zc_begin + 1));
+    load_v5(slice_rsrc(zc_begin - R));
     lds_barrier_abl<ABL>();
 
+    // ---- slice streams: descriptors advanced by one slice per step (two 32-bit adds each)
+    //      instead of rebuilt from z (a 64-bit multiply and range checks per descriptor) ------
+    // step i reads slice zb = i+1-R (leaving slice of P1(i+2), and v5), zb+R+1 = i+2 (Lc) and
+    // zb+2R+1 = i+2+R (entering slice of P1(i+2)); it stores output slice zs = i-1-R.
+    const int64_t sstride = p.in_sz * ESZ, osstride = p.out_sz * OSZ;
+    const int64_t off_c = (int64_t)(R + 1) * sstride, off_a = (int64_t)(2 * R + 1) * sstride;
+    int zb = zc_begin + 1 - R;
+    int64_t ob = (int64_t)(zb - p.in_z0) * sstride;
+    int zs = zc_begin - 1 - R;
+    int64_t os = (int64_t)(zs - p.oz0) * osstride;
+    const char* out_base = static_cast<const char*>(p.out);
+    const unsigned nzo = (unsigned)(zo_end - zo_begin);
+    auto rs_in = [&](int64_t off, int z) {
+        return make_rsrc(in_base + off, (unsigned)z < (unsigned)nz ? slice_bytes : 0u);
+    };
+
     // ---- pipelined march, unrolled by W so the ring slot of every P5 is a constant ----------
-    for (int i0 = zc_begin; i0 < zc_end; i0 += W) {
+    // The step count is padded to a multiple of W, at least one past the last stage-1 slice so
+    // that P5/the store of the last output slice happen inside the loop: no guards inside.
+    // Padded steps emit nothing (zo >= zo_end).
+    const int n_steps = (zc_end - zc_begin + 1 + W - 1) / W * W;
+    for (int i0 = zc_begin; i0 < zc_begin + n_steps; i0 += W) {
         static_for<0, W>([&](auto kc) {
             constexpr int k = decltype(kc)::value;
             const int i = i0 + k;
-            if (i >= zc_end) return;
             const int tid = threadIdx.x;
-            const bool has_next = i + 1 < zc_end;
-            // C0: P3(i) + P1(i+1) + P5(i-1)
+            const rsrc_t r_b = rs_in(ob, zb);
+            // C0: P3(i) + P1(i+1) + P5(i-1), then P1's loads for step i+2 (their latency
+            // hides under C1, the barriers and the next C0's P3)
             do_p3(tid, i);
-            if (has_next) do_p1(tid);
+            do_p1(tid);
             if (i > zc_begin) do_p5(tid, i - 1, std::integral_constant<int, (k + W - 1) % W>{});
-            // loads for the next iteration's C0 (latency hides under C1 and the barriers)
-            if (i + 2 < zc_end) load_p1(i + 2);
-            if (has_next) load_v3(tid, i + 1);
-            load_v5(tid, i - R);
+            load_p1(rs_in(ob + off_a, zb + 2 * R + 1), r_b);
             lds_barrier_abl<ABL>();
-            // C1: P4(i) + P2(i+1)
+            // C1: P4(i) + P2(i+1) + staging (stores of out(i-1-R), Lc(i+1), Lv5(i-R))
             do_p4(tid);
-            if (has_next) do_p2(tid);
+            do_p2(tid);
+            store_out(tid, make_rsrc(out_base + os,
+                                     (unsigned)(zs - zo_begin) < nzo ? oslice_bytes : 0u));
+            write_c(tid);
+            write_v5(tid);
+            load_c(rs_in(ob + off_c, zb + R + 1));
+            load_v5(r_b);
             lds_barrier_abl<ABL>();
+            ++zb;
+            ob += sstride;
+            ++zs;
+            os += osstride;
         });
     }
-    // ---- epilogue: stage 2 tail of the last slice (runtime slot -> dispatch, once) ----------
-    RingDispatch<0, W>::run((zc_end - 1 - zc_begin) % W, [&](auto slot_c) {
-        do_p5((int)threadIdx.x, zc_end - 1, slot_c);
-    });
 }
 
 // ---------------------------------------------------------------------------------------------
 // Launch: pick the tile configuration for the radius, dispatch dtypes.
 // ---------------------------------------------------------------------------------------------
-template <int R, int TY, int NT, typename TIn, typename TOut>
+inline long long floor_div(long long a, long long b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
+inline long long ceil_div(long long a, long long b) { return -floor_div(-a, b); }
+
+// Interior tile range along one axis: tiles t with origin o0 + t*T such that the whole E2 apron
+// [o0 + t*T - 2R, o0 + t*T + T + 2R + slack) is inside [0, n) and the output tile inside
+// [o0, o_end). Returns [lo, hi) (empty when lo >= hi).
+inline void interior_tiles(long long o0, long long o_end, long long n, int T, int R, int slack,
+                           int ntiles, int& lo, int& hi) {
+    long long l = ceil_div(2LL * R - o0, T);
+    long long h = floor_div(std::min(n - 2LL * R - slack, o_end) - T - o0, T) + 1;
+    l = std::max(l, 0LL);
+    h = std::min(h, (long long)ntiles);
+    if (h < l) h = l;
+    lo = (int)l;
+    hi = (int)h;
+}
+
+template <int R, int TY, int NT, typename TIn, typename TOut, bool EDGE, int ABL = 0>
+inline hipError_t launch_fused_variant(const GFParams& p, long long nwg, hipStream_t stream) {
+    using C = GFConfig<R, TY, NT>;
+    const size_t lds = (size_t)C::LDS_BYTES;
+    auto kern = gf3d_fused_kernel<R, TY, NT, TIn, TOut, EDGE, ABL>;
+    static bool attr_set = false;  // per instantiation
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute((const void*)kern,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+        attr_set = true;
+    }
+    if (nwg <= 0) return hipSuccess;
+    if (nwg > 0x7FFFFFFFLL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(NT), lds, stream, p);
+    return hipGetLastError();
+}
+
+template <int R, int TY, int NT, typename TIn, typename TOut, int ABL = 0>
 inline hipError_t launch_fused_cfg(const GFParams& p0, hipStream_t stream) {
     using C = GFConfig<R, TY, NT>;
     GFParams p = p0;
@@ -644,20 +998,30 @@ inline hipError_t launch_fused_cfg(const GFParams& p0, hipStream_t stream) {
     p.tiles_x = (p.onx + C::TX - 1) / C::TX;
     p.tiles_y = (p.ony + TY - 1) / TY;
     p.nseg = (p.onz + p.zseg - 1) / p.zseg;
-    const size_t lds = (size_t)C::LDS_BYTES;
-    auto kern = gf3d_fused_kernel<R, TY, NT, TIn, TOut>;
-    static bool attr_set = false;  // per instantiation
-    if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)kern,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (e != hipSuccess) return e;
-        attr_set = true;
+    // Quad-aligned geometry: every quad starts at a multiple of 4 elements (the E2 apron at
+    // x0 - 2R, the output tile at x0), and the domain / output box widths are multiples of 4,
+    // so no quad straddles a boundary: the first kernel takes every tile.
+    const bool quad_ok = (p.ox0 % 4 == 0) && (R % 2 == 0) && (p.nx % 4 == 0) &&
+                         (p.onx % 4 == 0) && (p.in_sy % 4 == 0) && (p.in_sz % 4 == 0) &&
+                         (p.out_sy % 4 == 0) && (p.out_sz % 4 == 0) &&
+                         ((uintptr_t)p.in % (4 * sizeof(TIn)) == 0) &&
+                         ((uintptr_t)p.out % (4 * sizeof(TOut)) == 0);
+    if (quad_ok) {
+        p.itx0 = 0; p.itx1 = p.tiles_x;
+        p.ity0 = 0; p.ity1 = p.tiles_y;
+    } else {
+        // +4 elements of x slack: the last Lc quad of a row may overhang the E1 apron
+        interior_tiles(p.ox0, p.ox0 + p.onx, p.nx, C::TX, R, 4, p.tiles_x, p.itx0, p.itx1);
+        interior_tiles(p.oy0, p.oy0 + p.ony, p.ny, TY, R, 0, p.tiles_y, p.ity0, p.ity1);
     }
-    const long long nwg = (long long)p.tiles_x * p.tiles_y * p.nseg;
-    if (nwg <= 0) return hipSuccess;
-    if (nwg > 0x7FFFFFFFLL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(NT), lds, stream, p);
-    return hipGetLastError();
+    const long long n_int = (long long)(p.itx1 - p.itx0) * (p.ity1 - p.ity0);
+    const long long n_all = (long long)p.tiles_x * p.tiles_y;
+    hipError_t e = hipSuccess;
+    if (n_int > 0)
+        e = launch_fused_variant<R, TY, NT, TIn, TOut, false, ABL>(p, n_int * p.nseg, stream);
+    if (e == hipSuccess && n_all > n_int)
+        e = launch_fused_variant<R, TY, NT, TIn, TOut, true, ABL>(p, n_all * p.nseg, stream);
+    return e;
 }
 
 

@@ -26,6 +26,7 @@ struct GFParams {
     int onz, ony, onx;
     int zseg;  // output slices per workgroup march (normally the chunk depth)
     int tiles_x, tiles_y, nseg;
+    int itx0, itx1, ity0, ity1;  // interior tile range (fused kernel, host-computed)
     float eps;
     float rcp_w3;  // RN(1 / (2r+1)^3): the interior window count's reciprocal (host-computed)
 };
