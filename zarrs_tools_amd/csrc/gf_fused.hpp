@@ -308,6 +308,18 @@ template <> struct Buf<uint8_t> {
     }
 };
 
+// ---- DPP wave shifts of an f64 (lane i <- lane i-1 / i+1; GFX9 wave_shr:1 / wave_shl:1) ----
+__device__ __forceinline__ double dpp_from_lower(double v) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x138, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x138, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double dpp_from_upper(double v) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x130, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x130, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+
 // ---- 4 consecutive elements (one 16/8/4-byte buffer access per lane) ----------------------
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
@@ -389,32 +401,33 @@ struct GFConfig {
     // Pitches in 8-byte elements, = 2 mod 4: 16-B aligned rows and conflict-free ds_*_b128
     // when lanes walk rows (16-lane groups land on distinct 4-bank slots).
     static constexpr int p2m4(int x) { return x + ((2 - x % 4) + 4) % 4; }
-    static constexpr int PV = p2m4(E2X);  // Lv  (f64)    P1 writes, P2 reads rows
-    static constexpr int PH = p2m4(E1X);  // Hx  (f64)    P2 writes rows, P3 reads columns
+    static constexpr int PH = p2m4(E1X);  // Hx  (f64)    P12 writes rows, P3 reads columns
     static constexpr int PA = p2m4(E1X);  // Lab (float2) P3 writes, P4 reads rows
     static constexpr int PB = p2m4(TX);   // Hab (float2) P4 writes rows, P5 reads columns
-    static constexpr int K2 = 4, K3 = 4, K4 = 4;
+    static constexpr int K3 = 4, K4 = 4;
     static constexpr int K5 = TX * TY / NT;          // outputs per thread (ring width)
-    static constexpr int S2 = (E1X + K2 - 1) / K2;   // segments per row, P2
     static constexpr int S3 = (E1Y + K3 - 1) / K3;   // segments per column, P3
     static constexpr int S4 = TX / K4;               // segments per row, P4
-    static constexpr int N2 = E2Y * S2, N3 = E1X * S3, N4 = E1Y * S4;  // work items
-    // quads (4 consecutive x) of the global accesses
-    static constexpr int NQ1X = E2X / 4, NQ1 = NQ1X * E2Y;   // P1: the E2 apron
-    static constexpr int NQP1 = (NQ1 + NT - 1) / NT;         // P1 quads per thread
+    static constexpr int N3 = E1X * S3, N4 = E1Y * S4;  // work items
+    // P12: one lane per quad (4 consecutive x) of an E2 row, whole rows per wave, so the
+    // x-neighbour quads of the window sums come from adjacent lanes (DPP), never across waves
+    static constexpr int NQ1X = E2X / 4;                   // quads per E2 row
+    static constexpr int RPW = 64 / NQ1X;                  // E2 rows per wave
+    static constexpr int NWAVE = NT / 64;
+    static constexpr int NQP1 = (E2Y + RPW * NWAVE - 1) / (RPW * NWAVE);  // passes
+    static constexpr int NB = (R + 3) / 4;                 // neighbour quads on each side
     static constexpr int XC = R % 4;  // Lc quad grid starts XC elements left of the E1 apron
     static constexpr int NQCX = (E1X + XC + 3) / 4, NQC = NQCX * E1Y;  // Lc: the E1 apron
     static constexpr int PC = 4 * NQCX;                      // Lc pitch (floats)
     static constexpr int NQ5 = TX / 4 * TY;                  // v5 / output tile quads
     static constexpr int W3 = W * W * W;                     // interior window count
     static constexpr int al(int b) { return (b + 255) / 256 * 256; }
-    static constexpr int SZ_LV = al((E2Y + 1) * PV * 8);
     static constexpr int SZ_HX = al((E2Y + K3) * PH * 8);
     static constexpr int SZ_LAB = al((E1Y + 1) * PA * 8);
     static constexpr int SZ_HAB = al((E1Y + 1) * PB * 8);
     static constexpr int SZ_LC = al(E1Y * PC * 4);
     static constexpr int SZ_T = al(TY * TX * 4);
-    static constexpr int OFF_HX = SZ_LV, OFF_LAB = OFF_HX + SZ_HX, OFF_HAB = OFF_LAB + SZ_LAB;
+    static constexpr int OFF_HX = 0, OFF_LAB = OFF_HX + SZ_HX, OFF_HAB = OFF_LAB + SZ_LAB;
     static constexpr int OFF_LC = OFF_HAB + SZ_HAB, OFF_LV5 = OFF_LC + SZ_LC;
     static constexpr int OFF_LOUT = OFF_LV5 + SZ_T, OFF_RCP = OFF_LOUT + SZ_T;
     static constexpr int SZ_RCP = al((W3 + 1) * 4);  // RN(1/c) for window counts c <= W^3
@@ -422,11 +435,11 @@ struct GFConfig {
     static constexpr int LDS_BYTES = OFF_DUMMY + 256;
     // item -> thread placement: heavy phases on different waves (see C0 / C1)
     static constexpr int T3 = NT - N3;  // P3 items on the top threads
-    static constexpr int T2 = NT - N2;  // P2 items on the top threads, P4 on the bottom
     static_assert(TX * TY % NT == 0, "tile must divide evenly over the threads");
     static_assert(TY % K5 == 0, "ring segment must divide the tile height");
     static_assert(TX % K4 == 0, "P4 segment must divide the tile width");
-    static_assert(N2 <= NT && N3 <= NT && N4 <= NT, "one work item per thread per phase");
+    static_assert(N3 <= NT && N4 <= NT, "one work item per thread per phase");
+    static_assert(RPW >= 1, "an E2 row fits one wave");
     static_assert(NQC <= NT && NQ5 <= NT, "one staging quad per thread");
     static_assert(E2X % 4 == 0, "E2 rows are whole quads");
     static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
@@ -446,7 +459,6 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     constexpr int K5 = C::K5;
     constexpr int ESZ = (int)sizeof(TIn), OSZ = (int)sizeof(TOut);
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    double* Lv = reinterpret_cast<double*>(smem);
     double* Hx = reinterpret_cast<double*>(smem + C::OFF_HX);
     float2* Lab = reinterpret_cast<float2*>(smem + C::OFF_LAB);
     float2* Hab = reinterpret_cast<float2*>(smem + C::OFF_HAB);
@@ -529,18 +541,25 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     // ---- per-thread, step-invariant quad offsets and in-domain masks -----------------------
     const int tid0 = threadIdx.x;
     int q1off[C::NQP1], q1mask[C::NQP1];
+    // P12 lane -> (E2 row, quad) for pass k
+    auto p12_pos = [&](int tid, int k, int& row, int& cq) -> bool {
+        const int w = tid / 64, l = tid % 64;
+        row = (k * C::NWAVE + w) * C::RPW + l / C::NQ1X;
+        cq = l % C::NQ1X;
+        return l < C::RPW * C::NQ1X && row < C::E2Y;
+    };
 #pragma unroll
     for (int k = 0; k < C::NQP1; ++k) {
-        const int q = tid0 + k * NT;
-        const int row = q / C::NQ1X, cq = q % C::NQ1X;
+        int row, cq;
+        const bool valid = p12_pos(tid0, k, row, cq);
         const int gx = x0 - 2 * R + 4 * cq, gy = y0 - 2 * R + row;
         int m = 0;
-        if (q < C::NQ1 && gy >= 0 && gy < ny) {
+        if (valid && gy >= 0 && gy < ny) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) m |= (gx + e >= 0 && gx + e < nx) ? (1 << e) : 0;
         }
         q1mask[k] = m;
-        q1off[k] = (EDGE ? q < C::NQ1 : m == 0xF) ? (gy * sy + gx) * ESZ : kBadOff;
+        q1off[k] = (EDGE ? valid : m == 0xF) ? (gy * sy + gx) * ESZ : kBadOff;
     }
     // Lc / v5 / output quads: offsets and masks are recomputed at their one use per step
     // (a few integer ops) rather than held in registers across the march.
@@ -615,42 +634,40 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
             else load_quad(rs, q1off[k], q1mask[k], ps[k]);
         }
     };
-    auto do_p1 = [&](int tid) {  // z-window of v (f64) on the E2 apron -> Lv
+    // P12: z-window of v (f64, running) and its x-window sums on the E2 apron -> Hx. The x
+    // neighbours come from the adjacent lanes' quads by DPP wave shifts (whole rows per wave),
+    // so the z-window never goes through LDS.
+    auto do_p12 = [&](int tid) {
 #pragma unroll
         for (int k = 0; k < C::NQP1; ++k) {
-            const int q = tid + k * NT;
-            const int row = q / C::NQ1X, cq = q % C::NQ1X;
+            int row, cq;
+            const bool valid = p12_pos(tid, k, row, cq);
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 zv[k][e] = zv[k][e] + (double)pa[k][e];  // entering slice (0 outside the domain)
                 zv[k][e] = zv[k][e] - (double)ps[k][e];  // leaving slice (0 outside the domain)
             }
-            if (q < C::NQ1) {
-                double2* dst = reinterpret_cast<double2*>(Lv + row * C::PV + 4 * cq);
-                dst[0] = make_double2(zv[k][0], zv[k][1]);
-                dst[1] = make_double2(zv[k][2], zv[k][3]);
+            constexpr int NB = C::NB;
+            double win[4 * (2 * NB + 1)];  // quads q-NB .. q+NB
+#pragma unroll
+            for (int e = 0; e < 4; ++e) win[4 * NB + e] = zv[k][e];
+#pragma unroll
+            for (int n = 1; n <= NB; ++n)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    win[4 * (NB - n) + e] = dpp_from_lower(win[4 * (NB - n + 1) + e]);
+                    win[4 * (NB + n) + e] = dpp_from_upper(win[4 * (NB + n - 1) + e]);
+                }
+            double vin[4 + 2 * R], hs[4];
+#pragma unroll
+            for (int j = 0; j < 4 + 2 * R; ++j) vin[j] = win[4 * NB - R + j];
+            slide_sums_f64<R, 4>(vin, hs);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int col = 4 * cq + e - R;  // Hx column (x - (x0 - R))
+                if (valid && col >= 0 && col < C::E1X) Hx[row * C::PH + col] = hs[e];
             }
         }
-    };
-    auto do_p2 = [&](int tid) {  // x-window sums (f64) of Lv rows -> Hx
-        const int item = tid - C::T2;
-        if (item < 0) return;
-        const int row = item % C::E2Y, sg = item / C::E2Y;
-        const double2* src =
-            reinterpret_cast<const double2*>(Lv + row * C::PV + sg * C::K2);
-        double vin[C::K2 + 2 * R], vout[C::K2];
-#pragma unroll
-        for (int j = 0; j < (C::K2 + 2 * R) / 2; ++j) {
-            const double2 d2 = src[j];
-            vin[2 * j] = d2.x;
-            vin[2 * j + 1] = d2.y;
-        }
-        if constexpr ((C::K2 + 2 * R) % 2) vin[C::K2 + 2 * R - 1] = Lv[row * C::PV + sg * C::K2 + C::K2 + 2 * R - 1];
-        slide_sums_f64<R, C::K2>(vin, vout);
-        double2* dst = reinterpret_cast<double2*>(Hx + row * C::PH + sg * C::K2);
-#pragma unroll
-        for (int j = 0; j < C::K2 / 2; ++j)
-            if (sg * C::K2 + 2 * j < C::E1X) dst[j] = make_double2(vout[2 * j], vout[2 * j + 1]);
     };
     // Pointwise stage on NP pairs of E1 positions, packed (both lanes of every op in one issue)
     // and written op-by-op across the pairs so dependent packed ops are interleaved (gfx950
@@ -884,16 +901,14 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
         else Quad<TOut>::store(o, ro, off);
     };
 
-    // ---- prologue: stage 1 of the first slice up to Hx, first Lc ---------------------------
+    // ---- prologue: stage 1 of the first slice up to Hx, first Lc; prefetch step 1 -----------
     load_p1(slice_rsrc(zc_begin + R), slice_rsrc(zc_begin - R - 1));
     load_c(slice_rsrc(zc_begin));
-    do_p1(tid0);
+    do_p12(tid0);
     write_c(tid0);
-    lds_barrier_abl<ABL>();
-    do_p2(tid0);
-    load_p1(slice_rsrc(zc_begin + 1 + R), slice_rsrc(zc_begin - R));
     load_c(slice_rsrc(zc_begin + 1));
     load_v5(slice_rsrc(zc_begin - R));
+    load_p1(slice_rsrc(zc_begin + 1 + R), slice_rsrc(zc_begin - R));
     lds_barrier_abl<ABL>();
 
     // ---- slice streams: descriptors advanced by one slice per step (two 32-bit adds each)
@@ -923,22 +938,21 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
             const int i = i0 + k;
             const int tid = threadIdx.x;
             const rsrc_t r_b = rs_in(ob, zb);
-            // C0: P3(i) + P1(i+1) + P5(i-1), then P1's loads for step i+2 (their latency
-            // hides under C1, the barriers and the next C0's P3)
+            // C0: P3(i) + P5(i-1) (LDS and registers only)
             do_p3(tid, i);
-            do_p1(tid);
             if (i > zc_begin) do_p5(tid, i - 1, std::integral_constant<int, (k + W - 1) % W>{});
-            load_p1(rs_in(ob + off_a, zb + 2 * R + 1), r_b);
             lds_barrier_abl<ABL>();
-            // C1: P4(i) + P2(i+1) + staging (stores of out(i-1-R), Lc(i+1), Lv5(i-R))
-            do_p4(tid);
-            do_p2(tid);
+            // C1: staging (store out(i-1-R), Lc <- slice i+1, Lv5 <- slice i-R), the loads of
+            // the next step, P12(i+1), P4(i). Every wait here is for a load issued a step ago.
             store_out(tid, make_rsrc(out_base + os,
                                      (unsigned)(zs - zo_begin) < nzo ? oslice_bytes : 0u));
             write_c(tid);
             write_v5(tid);
             load_c(rs_in(ob + off_c, zb + R + 1));
             load_v5(r_b);
+            do_p12(tid);
+            load_p1(rs_in(ob + off_a, zb + 2 * R + 1), r_b);
+            do_p4(tid);
             lds_barrier_abl<ABL>();
             ++zb;
             ob += sstride;
