@@ -9,10 +9,10 @@ mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$ROOT/$OUT/trace" -o run --output-format csv \
   -- python3 "$ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline > "$ROOT/$OUT/trace.log" 2>&1
-echo "trace rc=$?"
+rc=$?; echo "trace rc=$rc"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$ROOT/$OUT/fetch" -o run --output-format csv \
   -- python3 "$ROOT/bench.py" --steps 1 --warmup 0 --no-cpu-baseline > "$ROOT/$OUT/fetch.log" 2>&1
-echo "fetch rc=$?"
+rc=$?; echo "fetch rc=$rc"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$ROOT/$OUT/write" -o run --output-format csv \
   -- python3 "$ROOT/bench.py" --steps 1 --warmup 0 --no-cpu-baseline > "$ROOT/$OUT/write.log" 2>&1
-echo "write rc=$?"
+rc=$?; echo "write rc=$rc"; [ $rc -eq 0 ] || exit $rc
