@@ -184,6 +184,72 @@ int zt_synth_step_noise_f32(zt_ctx* ctx, float* out, const int64_t* shape, int n
 int zt_synth_u16(zt_ctx* ctx, uint16_t* out, const int64_t* shape, int ndim,
                  const int64_t* global_shape, int64_t z0, uint64_t seed);
 
+
+/* ---- Zarr V3 store -> store path (host storage in and out) ----------------------------------
+ * The reference's filters read and write Zarr arrays through zarrs (Array::retrieve_array_subset_
+ * ndarray / store_array_subset_ndarray, guided_filter.rs:95-110; zarrs_ome.rs:226-232). These
+ * entry points restate that I/O for filesystem stores (zarr.json V3 metadata, regular chunk grid,
+ * default/v2 chunk keys, codecs bytes, gzip, zstd (runtime libzstd.so.1), crc32c and
+ * sharding_indexed) and drive the device kernels over it with a pipelined chunk-row loop:
+ * decode (host threads) -> H2D -> kernel -> D2H -> encode (host threads), each input chunk
+ * decoded once. Host buffers here are ordinary host memory. */
+
+/* Per-call statistics (the reference's Progress read/process/write split, progress.rs:15-105,
+ * plus the device phases). *_s of host phases are thread-seconds; device phases are event
+ * seconds summed over chunk rows; wall_s is the whole call. */
+typedef struct zt_store_stats {
+    double wall_s;
+    double decode_s, encode_s;         /* host thread-seconds: read+decode, encode+write */
+    double h2d_s, kernel_s, d2h_s;     /* device seconds */
+    uint64_t bytes_read, bytes_written;/* encoded bytes moved to/from storage */
+    uint64_t voxels;                   /* output elements produced */
+    int64_t rows;                      /* output chunk rows processed */
+    int threads;                       /* host worker threads used */
+} zt_store_stats;
+
+/* flags for the store filters */
+#define ZT_STORE_ERASE_OUTPUT_METADATA 1 /* remove OUT/zarr.json first ("not finished" marker,
+                                             zarrs_filter.rs:297-300) */
+#define ZT_STORE_FINISH_OUTPUT 2         /* write OUT/zarr.json at the end (zarrs_filter.rs:313) */
+
+/* Array metadata of a Zarr V3 array: data type (zt_dtype), rank, shape, chunk (= shard) shape and
+ * the inner chunk shape of a sharded array (= chunk shape otherwise). Arrays of ZT_MAX_DIMS. */
+int zt_store_array_info(const char* path, int* dtype, int* ndim, int64_t* shape,
+                        int64_t* chunk_shape, int64_t* inner_chunk_shape);
+/* Create an array and write its zarr.json. codecs_json: a Zarr V3 codec list (NULL = [bytes,
+ * little endian]); fill_value_json: Zarr V3 fill_value JSON (NULL = 0 / false / 0.0). */
+int zt_store_create_array(const char* path, int dtype, int ndim, const int64_t* shape,
+                          const int64_t* chunk_shape, const char* codecs_json,
+                          const char* fill_value_json);
+/* The output array the filters create: the input's shape, chunking and codecs with data type
+ * dtype_out (-1 = the input's) and the input fill value cast to it (filter_traits.rs:47-82). */
+int zt_store_create_output_like(const char* in_path, const char* out_path, int dtype_out);
+/* Read any subset into a C-order host buffer (missing chunks read as the fill value). */
+int zt_store_read_subset(const char* path, const int64_t* start, const int64_t* shape,
+                         void* host_out, int nthreads);
+/* Write a chunk-aligned subset (may end at the array edge) from a C-order host buffer. */
+int zt_store_write_subset(const char* path, const int64_t* start, const int64_t* shape,
+                          const void* host_in, int nthreads);
+/* Fill an existing array with the SURVEY.md §8(d) synthetic data (kind 0: float32 step+noise,
+ * kind 1: uint16 noise), identical to zt_synth_step_noise_f32 / zt_synth_u16. */
+int zt_store_write_synth(const char* path, int kind, uint64_t seed, int nthreads);
+
+/* zarrs_filter guided-filter IN OUT EPS R [--data-type T] over a store (GuidedFilter::apply,
+ * guided_filter.rs:240-319): the output array is IN's shape/chunking/codecs with dtype_out (-1 =
+ * input type). Processes the output chunk rows [row_begin, row_end) along axis 0 (row_end < 0 =
+ * all), so ranks can split the rows; the array's zarr.json is written only with
+ * ZT_STORE_FINISH_OUTPUT. nthreads <= 0: min(16, hardware threads). stats may be NULL. */
+int zt_store_guided_filter(const char* in_path, const char* out_path, int dtype_out,
+                           float epsilon, int radius, int device, int64_t row_begin,
+                           int64_t row_end, int nthreads, int flags, zt_store_stats* stats);
+/* zarrs_filter downsample / one zarrs_ome level over a store (Downsample::apply,
+ * downsample.rs:170-286; output chunk = min(input chunk, output shape), zarrs_ome.rs:549-559). */
+int zt_store_downsample(const char* in_path, const char* out_path, const int64_t* stride,
+                        int discrete, int dtype_out, int device, int64_t row_begin,
+                        int64_t row_end, int nthreads, int flags, zt_store_stats* stats);
+/* 1 if the named codec can be read and written here, else 0. */
+int zt_store_codec_available(const char* name);
+
 #ifdef __cplusplus
 }
 #endif

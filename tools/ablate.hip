@@ -40,7 +40,7 @@ int main(int argc, char** argv) {
                                              hipMemcpyHostToDevice));
     GFParams p{};
     p.in = in; p.out = out; p.in_sz = (int64_t)n * n; p.in_sy = n; p.out_sz = (int64_t)n * n;
-    p.out_sy = n; p.in_z0 = 0; p.nz = p.ny = p.nx = n; p.oz0 = p.oy0 = p.ox0 = 0;
+    p.out_sy = n; p.in_z0 = 0; p.zlo = 0; p.zhi = n; p.nz = p.ny = p.nx = n; p.oz0 = p.oy0 = p.ox0 = 0;
     p.onz = p.ony = p.onx = n; p.zseg = 256; p.eps = 2500.0f;
     hipStream_t s; CK(hipStreamCreate(&s));
     const char* names[] = {"full", "no leave load (1)", "no Lc load (2)", "no v5 load (4)",

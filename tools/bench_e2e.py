@@ -1,0 +1,87 @@
+#!/usr/bin/env python3
+"""End-to-end (store -> store) guided filter rate: a Zarr V3 store on host storage in, a Zarr V3
+store out, chunk decode -> H2D -> HIP kernel -> D2H -> chunk encode pipelined (zt_store_guided_
+filter). Prints one JSON line. The input store is written first (not timed) and is therefore in
+the host page cache: the rate is "warm page cache" (no drop_caches without root).
+
+A sample of the output (the first chunk row) is checked against the oracle (test
+infrastructure, never timed): planes [0, c) of the output depend only on input planes [0, c+2r),
+so the oracle run on that block gives the reference's values for them.
+"""
+import argparse
+import json
+import os
+import shutil
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--size", type=int, default=1024)
+    ap.add_argument("--chunk", type=int, default=256)
+    ap.add_argument("--radius", type=int, default=2)
+    ap.add_argument("--eps", type=float, default=2500.0)
+    ap.add_argument("--codec", default="bytes", choices=["bytes", "gzip", "zstd"])
+    ap.add_argument("--level", type=int, default=1)
+    ap.add_argument("--shard-inner", type=int, default=0, help="sharded store, inner chunk edge")
+    ap.add_argument("--dir", default=os.environ.get("TMPDIR", "/tmp"))
+    ap.add_argument("--threads", type=int, default=16)
+    ap.add_argument("--repeat", type=int, default=2)
+    ap.add_argument("--check", type=int, default=1)
+    ap.add_argument("--keep", action="store_true")
+    a = ap.parse_args()
+
+    from zarrs_tools_amd import store as S
+    work = os.path.join(a.dir, f"zt_e2e_{os.getpid()}")
+    os.makedirs(work, exist_ok=True)
+    pin, pout = os.path.join(work, "in.zarr"), os.path.join(work, "out.zarr")
+    shape, chunk = (a.size,) * 3, (a.chunk,) * 3
+    comp = None if a.codec == "bytes" else a.codec
+    codecs = S.codecs_json(comp, a.level, (a.shard_inner,) * 3 if a.shard_inner else None)
+    try:
+        t0 = time.perf_counter()
+        S.create_array(pin, "float32", shape, chunk, codecs)
+        S.write_synth(pin, S.SYNTH_STEP_NOISE_F32, nthreads=a.threads)
+        t_make = time.perf_counter() - t0
+        stats = []
+        for _ in range(a.repeat):
+            stats.append(S.guided_filter(pin, pout, a.eps, a.radius, nthreads=a.threads))
+        best = min(stats, key=lambda s: s["wall_s"])
+        vox = best["voxels"]
+        res = {
+            "metric": "GiB/s filtered end-to-end (Zarr V3 store -> store, warm page cache)",
+            "value": round(vox * 4 / 2 ** 30 / best["wall_s"], 3),
+            "unit": "GiB/s",
+            "config": {"shape": shape, "chunk": chunk, "radius": a.radius, "eps": a.eps,
+                       "codec": a.codec, "level": a.level, "shard_inner": a.shard_inner,
+                       "host_threads": best["threads"]},
+            "wall_s": round(best["wall_s"], 3),
+            "phases": {k: round(best[k], 3) for k in
+                       ("decode_s", "encode_s", "h2d_s", "kernel_s", "d2h_s")},
+            "bytes_read": best["bytes_read"], "bytes_written": best["bytes_written"],
+            "input_store_bytes_per_s": round(best["bytes_read"] / best["wall_s"] / 1e9, 3),
+            "walls": [round(s["wall_s"], 3) for s in stats],
+            "make_input_s": round(t_make, 2),
+        }
+        if a.check:
+            import numpy as np
+            from oracle import oracle as O
+            c = a.chunk
+            block = S.read_array(pin, (0, 0, 0), (min(c + 2 * a.radius, a.size), a.size, a.size))
+            got = S.read_array(pout, (0, 0, 0), (c, a.size, a.size))
+            ref = O.guided_filter_apply_ndarray(block, a.eps, a.radius)[:c]
+            err = float(np.max(np.abs(got.astype(np.float64) - ref) /
+                               np.maximum(1.0, np.abs(ref))))
+            res["check"] = {"planes": c, "max_rel_err": err, "ok": err <= 1e-5}
+        print(json.dumps(res), flush=True)
+    finally:
+        if not a.keep:
+            shutil.rmtree(work, ignore_errors=True)
+
+
+if __name__ == "__main__":
+    main()

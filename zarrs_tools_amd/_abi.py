@@ -64,6 +64,22 @@ _STATUS_CLASS = {
 
 _lib = None
 
+# flags of the store filters
+STORE_ERASE_OUTPUT_METADATA = 1
+STORE_FINISH_OUTPUT = 2
+
+
+class StoreStats(ctypes.Structure):
+    """zt_store_stats (include/zarrs_tools_amd.h)."""
+    _fields_ = [("wall_s", ctypes.c_double), ("decode_s", ctypes.c_double),
+                ("encode_s", ctypes.c_double), ("h2d_s", ctypes.c_double),
+                ("kernel_s", ctypes.c_double), ("d2h_s", ctypes.c_double),
+                ("bytes_read", ctypes.c_uint64), ("bytes_written", ctypes.c_uint64),
+                ("voxels", ctypes.c_uint64), ("rows", ctypes.c_int64), ("threads", ctypes.c_int)]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
 
 def header_symbols() -> list[str]:
     """Every function name declared in include/zarrs_tools_amd.h."""
@@ -125,6 +141,22 @@ def lib() -> ctypes.CDLL:
         "zt_synth_step_noise_f32": ([vp, vp, i64p, c_int, i64p, ctypes.c_int64, ctypes.c_uint64],
                                     c_int),
         "zt_synth_u16": ([vp, vp, i64p, c_int, i64p, ctypes.c_int64, ctypes.c_uint64], c_int),
+        # store -> store path (host storage)
+        "zt_store_array_info": ([ctypes.c_char_p, ctypes.POINTER(c_int), ctypes.POINTER(c_int),
+                                 i64p, i64p, i64p], c_int),
+        "zt_store_create_array": ([ctypes.c_char_p, c_int, c_int, i64p, i64p, ctypes.c_char_p,
+                                   ctypes.c_char_p], c_int),
+        "zt_store_create_output_like": ([ctypes.c_char_p, ctypes.c_char_p, c_int], c_int),
+        "zt_store_read_subset": ([ctypes.c_char_p, i64p, i64p, vp, c_int], c_int),
+        "zt_store_write_subset": ([ctypes.c_char_p, i64p, i64p, vp, c_int], c_int),
+        "zt_store_write_synth": ([ctypes.c_char_p, c_int, ctypes.c_uint64, c_int], c_int),
+        "zt_store_guided_filter": ([ctypes.c_char_p, ctypes.c_char_p, c_int, c_float, c_int,
+                                    c_int, ctypes.c_int64, ctypes.c_int64, c_int, c_int,
+                                    ctypes.POINTER(StoreStats)], c_int),
+        "zt_store_downsample": ([ctypes.c_char_p, ctypes.c_char_p, i64p, c_int, c_int, c_int,
+                                 ctypes.c_int64, ctypes.c_int64, c_int, c_int,
+                                 ctypes.POINTER(StoreStats)], c_int),
+        "zt_store_codec_available": ([ctypes.c_char_p], c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

@@ -523,8 +523,11 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     const int sy = (int)p.in_sy, osy = (int)p.out_sy;  // 32-bit: slices < 2 GiB (host check)
 
     const char* in_base = static_cast<const char*>(p.in);
+    // Planes outside [zlo, zhi) (outside the domain, or outside a slab's rows) read as 0: a slab
+    // carries the 2r halo of its output rows, so they only feed steps that emit nothing.
+    const int zlo = p.zlo, zspan = p.zhi - p.zlo;
     auto slice_rsrc = [&](int z) -> rsrc_t {
-        const bool ok = z >= 0 && z < nz;
+        const bool ok = (unsigned)(z - zlo) < (unsigned)zspan;
         const char* base = in_base + (ok ? (int64_t)(z - p.in_z0) * p.in_sz * ESZ : 0);
         return make_rsrc(base, ok ? slice_bytes : 0u);
     };
@@ -602,8 +605,8 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     // clamped to [0, nz); every later step adds the entering and subtracts the leaving slice
     // (both 0 outside the domain), so the window stays exact through out-of-domain steps.
     {
-        const int zlo = max(zc_begin - 1 - R, 0), zhi = min(zc_begin - 1 + R, nz - 1);
-        for (int z = zlo; z <= zhi; ++z) {
+        const int za = max(zc_begin - 1 - R, 0), zb_ = min(zc_begin - 1 + R, nz - 1);
+        for (int z = za; z <= zb_; ++z) {
             const rsrc_t rs = slice_rsrc(z);
 #pragma unroll
             for (int k = 0; k < C::NQP1; ++k) {
@@ -924,7 +927,7 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     const char* out_base = static_cast<const char*>(p.out);
     const unsigned nzo = (unsigned)(zo_end - zo_begin);
     auto rs_in = [&](int64_t off, int z) {
-        return make_rsrc(in_base + off, (unsigned)z < (unsigned)nz ? slice_bytes : 0u);
+        return make_rsrc(in_base + off, (unsigned)(z - zlo) < (unsigned)zspan ? slice_bytes : 0u);
     };
 
     // ---- pipelined march, unrolled by W so the ring slot of every P5 is a constant ----------

@@ -1,0 +1,806 @@
+// zt_store.cpp — the store -> store path: Zarr V3 arrays on host storage in, Zarr V3 arrays out,
+// the per-chunk transform on the GPU in between (C ABI: include/zarrs_tools_amd.h, "store").
+//
+// Reference: GuidedFilter::apply / apply_chunk (guided_filter.rs:75-114, 240-319) read every
+// output chunk's 2r-halo subset from the input store (decoding up to 3^d input chunks per output
+// chunk), filter it on a rayon worker, and store the output chunk; zarrs_ome's level loop
+// (zarrs_ome.rs:515-738) does the same with Downsample. Here the chunk grid is walked in chunk
+// rows along axis 0, and the work is pipelined over host threads and three HIP streams:
+//
+//   decode row j+1.. (host pool)  |  H2D slab k -> kernel k -> D2H row k (GPU)  |  encode row k-1
+//
+// Each input chunk is decoded exactly once into a pinned host row buffer (a ring of rows); the
+// slab for output row k = the planes [z0 - 2r, z1 + 2r) is assembled on the device from the rows
+// that hold them, so the halo is shared instead of re-decoded. Output rows come back into a
+// double-buffered pinned host buffer and are encoded chunk by chunk on the pool.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <exception>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../../include/zarrs_tools_amd.h"
+#include "../zt_device.hpp"
+#include "zt_zarr.hpp"
+
+namespace zt {
+int set_last_error(int code, const char* msg);
+}
+
+namespace {
+
+using zt::zarr::Array;
+using Clock = std::chrono::steady_clock;
+
+double secs_since(Clock::time_point t0) {
+    return std::chrono::duration<double>(Clock::now() - t0).count();
+}
+
+// ---- a small fixed thread pool with task groups ------------------------------------------------
+class Group {
+  public:
+    void add() {
+        std::lock_guard<std::mutex> l(m_);
+        ++pending_;
+    }
+    void done(std::exception_ptr e) {
+        std::lock_guard<std::mutex> l(m_);
+        if (e && !err_) err_ = e;
+        if (--pending_ == 0) cv_.notify_all();
+    }
+    void wait() {
+        std::unique_lock<std::mutex> l(m_);
+        cv_.wait(l, [&] { return pending_ == 0; });
+        if (err_) {
+            std::exception_ptr e = err_;
+            err_ = nullptr;
+            std::rethrow_exception(e);
+        }
+    }
+    void wait_nothrow() {
+        std::unique_lock<std::mutex> l(m_);
+        cv_.wait(l, [&] { return pending_ == 0; });
+    }
+
+  private:
+    std::mutex m_;
+    std::condition_variable cv_;
+    int pending_ = 0;
+    std::exception_ptr err_;
+};
+
+class Pool {
+  public:
+    explicit Pool(int n) {
+        for (int i = 0; i < n; ++i) th_.emplace_back([this] { loop(); });
+    }
+    ~Pool() {
+        {
+            std::lock_guard<std::mutex> l(m_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    void submit(Group& g, std::function<void()> f) {
+        g.add();
+        {
+            std::lock_guard<std::mutex> l(m_);
+            q_.emplace_back([&g, f = std::move(f)] {
+                std::exception_ptr e;
+                try {
+                    f();
+                } catch (...) {
+                    e = std::current_exception();
+                }
+                g.done(e);
+            });
+        }
+        cv_.notify_one();
+    }
+    int size() const { return (int)th_.size(); }
+
+  private:
+    void loop() {
+        for (;;) {
+            std::function<void()> f;
+            {
+                std::unique_lock<std::mutex> l(m_);
+                cv_.wait(l, [&] { return stop_ || !q_.empty(); });
+                if (stop_ && q_.empty()) return;
+                f = std::move(q_.front());
+                q_.pop_front();
+            }
+            f();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::deque<std::function<void()>> q_;
+    std::mutex m_;
+    std::condition_variable cv_;
+    bool stop_ = false;
+};
+
+int resolve_threads(int n) {
+    if (n > 0) return n;
+    unsigned hc = std::thread::hardware_concurrency();
+    return (int)std::max(1u, std::min(hc ? hc : 8u, 16u));
+}
+
+std::vector<int64_t> c_strides(const std::vector<int64_t>& shape) {
+    std::vector<int64_t> st(shape.size());
+    int64_t s = 1;
+    for (int d = (int)shape.size() - 1; d >= 0; --d) { st[d] = s; s *= shape[d]; }
+    return st;
+}
+
+// every chunk index of the chunk rows [r0, r1) along axis 0
+std::vector<std::vector<int64_t>> chunks_in_rows(const Array& a, int64_t r0, int64_t r1) {
+    const auto g = a.grid_shape();
+    const int nd = a.ndim();
+    int64_t per = 1;
+    for (int d = 1; d < nd; ++d) per *= g[d];
+    std::vector<std::vector<int64_t>> out;
+    for (int64_t r = r0; r < r1; ++r)
+        for (int64_t c = 0; c < per; ++c) {
+            std::vector<int64_t> idx(nd);
+            idx[0] = r;
+            int64_t rem = c;
+            for (int d = nd - 1; d >= 1; --d) { idx[d] = rem % g[d]; rem /= g[d]; }
+            out.push_back(idx);
+        }
+    return out;
+}
+
+struct Pinned {
+    void* p = nullptr;
+    size_t n = 0;
+    void alloc(size_t bytes) {
+        n = bytes;
+        if (bytes && hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) {
+            (void)hipGetLastError();
+            p = nullptr;
+            throw zt::zarr::Error(ZT_ERR_OUT_OF_MEMORY, "pinned host allocation failed");
+        }
+    }
+    ~Pinned() {
+        if (p) (void)hipHostFree(p);
+    }
+    uint8_t* u8() const { return static_cast<uint8_t*>(p); }
+};
+
+struct DevBuf {
+    void* p = nullptr;
+    void alloc(size_t bytes) {
+        if (bytes && hipMalloc(&p, bytes) != hipSuccess) {
+            (void)hipGetLastError();
+            p = nullptr;
+            throw zt::zarr::Error(ZT_ERR_OUT_OF_MEMORY, "device allocation failed");
+        }
+    }
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+    uint8_t* u8() const { return static_cast<uint8_t*>(p); }
+};
+
+#define HIPCHK(x)                                                                                \
+    do {                                                                                         \
+        hipError_t _e = (x);                                                                     \
+        if (_e != hipSuccess)                                                                    \
+            throw zt::zarr::Error(ZT_ERR_DEVICE, std::string(#x) + ": " + hipGetErrorString(_e)); \
+    } while (0)
+
+struct Events {
+    std::vector<hipEvent_t> ev;
+    hipEvent_t make() {
+        hipEvent_t e;
+        HIPCHK(hipEventCreate(&e));
+        ev.push_back(e);
+        return e;
+    }
+    ~Events() {
+        for (auto e : ev) (void)hipEventDestroy(e);
+    }
+};
+
+struct Streams {
+    std::vector<hipStream_t> s;
+    hipStream_t make() {
+        hipStream_t x;
+        HIPCHK(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
+        s.push_back(x);
+        return x;
+    }
+    ~Streams() {
+        for (auto x : s) {
+            (void)hipStreamSynchronize(x);
+            (void)hipStreamDestroy(x);
+        }
+    }
+};
+
+struct Ctx {
+    zt_ctx* c = nullptr;
+    ~Ctx() {
+        if (c) zt_ctx_destroy(c);
+    }
+};
+
+float ev_ms(hipEvent_t a, hipEvent_t b) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, a, b) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0.f;
+    }
+    return ms;
+}
+
+uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ULL;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
+    return x ^ (x >> 31);
+}
+
+// Convert a fill value to another data type with Rust `as` semantics (lib.rs convert_fill_value).
+zt::json::Value convert_fill(const Array& a, int dtype_out) {
+    const uint8_t* f = a.fill.data();
+    double v = 0.0;
+    switch (a.dtype) {
+    case ZT_BOOL: case ZT_UINT8: v = f[0]; break;
+    case ZT_INT8: v = (int8_t)f[0]; break;
+    case ZT_INT16: { int16_t x; std::memcpy(&x, f, 2); v = x; break; }
+    case ZT_INT32: { int32_t x; std::memcpy(&x, f, 4); v = x; break; }
+    case ZT_INT64: { int64_t x; std::memcpy(&x, f, 8); v = (double)x; break; }
+    case ZT_UINT16: { uint16_t x; std::memcpy(&x, f, 2); v = x; break; }
+    case ZT_UINT32: { uint32_t x; std::memcpy(&x, f, 4); v = x; break; }
+    case ZT_UINT64: { uint64_t x; std::memcpy(&x, f, 8); v = (double)x; break; }
+    case ZT_BFLOAT16: { uint16_t x; std::memcpy(&x, f, 2); v = zt::bf16_bits_to_f32(x); break; }
+    case ZT_FLOAT16: { uint16_t x; std::memcpy(&x, f, 2); v = zt::f16_bits_to_f32(x); break; }
+    case ZT_FLOAT32: { float x; std::memcpy(&x, f, 4); v = x; break; }
+    case ZT_FLOAT64: std::memcpy(&v, f, 8); break;
+    }
+    if (dtype_out < ZT_BFLOAT16 && dtype_out != ZT_BOOL) {
+        if (std::isnan(v)) v = 0.0;  // `as` maps NaN to 0 for integers
+    }
+    return zt::zarr::fill_json_from_double(dtype_out, v);
+}
+
+int report(const std::exception& e) {
+    if (auto* z = dynamic_cast<const zt::zarr::Error*>(&e)) return zt::set_last_error(z->code, z->what());
+    return zt::set_last_error(ZT_ERR_OTHER, e.what());
+}
+
+// ---- the chunk-row pipeline --------------------------------------------------------------------
+
+// What one output chunk row needs from the input and how it is computed on the device.
+struct RowOp {
+    // input planes along axis 0 for output planes [z0, z1)
+    std::function<void(int64_t z0, int64_t z1, int64_t& in0, int64_t& in1)> input_planes;
+    // run the transform: slab (input planes [in0, in1)) -> out (output planes [z0, z1))
+    std::function<int(zt_ctx*, const void* slab, int64_t in0, int64_t in1, void* out, int64_t z0,
+                      int64_t z1)>
+        apply;
+};
+
+void run_pipeline(const Array& in, const Array& out, int device, int64_t row_begin,
+                  int64_t row_end, int nthreads, const RowOp& op, zt_store_stats* st) {
+    const auto t_start = Clock::now();
+    const int nd = in.ndim();
+    const int64_t in_cz = in.chunk_shape[0], out_cz = out.chunk_shape[0];
+    const int64_t nz_in = in.shape[0], nz_out = out.shape[0];
+    const int64_t out_rows = (nz_out + out_cz - 1) / out_cz;
+    row_begin = std::max<int64_t>(0, row_begin);
+    row_end = row_end < 0 ? out_rows : std::min(row_end, out_rows);
+    if (row_begin >= row_end) return;
+    int64_t in_plane = 1, out_plane = 1;
+    for (int d = 1; d < nd; ++d) in_plane *= in.shape[d];
+    for (int d = 1; d < out.ndim(); ++d) out_plane *= out.shape[d];
+    const size_t in_pb = (size_t)in_plane * in.esz, out_pb = (size_t)out_plane * out.esz;
+
+    // input row span of each output row, and the largest slab
+    auto span = [&](int64_t k, int64_t& in0, int64_t& in1, int64_t& j0, int64_t& j1) {
+        const int64_t z0 = k * out_cz, z1 = std::min(z0 + out_cz, nz_out);
+        op.input_planes(z0, z1, in0, in1);
+        j0 = in0 / in_cz;
+        j1 = (in1 - 1) / in_cz;
+    };
+    int64_t max_slab = 0, max_rows_per = 1;
+    for (int64_t k = row_begin; k < row_end; ++k) {
+        int64_t a, b, j0, j1;
+        span(k, a, b, j0, j1);
+        max_slab = std::max(max_slab, b - a);
+        max_rows_per = std::max(max_rows_per, j1 - j0 + 1);
+    }
+    const int64_t NR = max_rows_per + 2;  // ring of decoded input rows (+1 decoding ahead, +1 slack)
+
+    if (hipSetDevice(device) != hipSuccess)
+        throw zt::zarr::Error(ZT_ERR_DEVICE, "hipSetDevice failed");
+    Ctx ctx;
+    if (int rc = zt_ctx_create(device, &ctx.c)) throw zt::zarr::Error(rc, zt_last_error());
+    Streams streams;
+    hipStream_t s_h2d = streams.make(), s_comp = streams.make(), s_d2h = streams.make();
+    if (int rc = zt_ctx_set_stream(ctx.c, s_comp)) throw zt::zarr::Error(rc, zt_last_error());
+    Events E;
+    hipEvent_t ev_h2d0[2], ev_h2d[2], ev_k0[2], ev_k[2], ev_d2h0[2], ev_d2h[2];
+    for (int s = 0; s < 2; ++s) {
+        ev_h2d0[s] = E.make(); ev_h2d[s] = E.make(); ev_k0[s] = E.make(); ev_k[s] = E.make();
+        ev_d2h0[s] = E.make(); ev_d2h[s] = E.make();
+    }
+    std::vector<hipEvent_t> ring_ev(NR);
+    std::vector<bool> ring_ev_set(NR, false);
+    for (auto& e : ring_ev) e = E.make();
+
+    std::vector<Pinned> hin(NR);
+    for (auto& h : hin) h.alloc((size_t)in_cz * in_pb);
+    Pinned hout[2];
+    for (auto& h : hout) h.alloc((size_t)out_cz * out_pb);
+    DevBuf dslab[2], dout[2];
+    for (int s = 0; s < 2; ++s) {
+        dslab[s].alloc((size_t)max_slab * in_pb);
+        dout[s].alloc((size_t)out_cz * out_pb);
+    }
+
+    Pool pool(resolve_threads(nthreads));
+    std::vector<Group> dec_group(NR);
+    Group enc_group[2];
+    std::vector<int64_t> ring_row(NR, -1);
+    std::atomic<uint64_t> bytes_read{0}, bytes_written{0};
+    std::atomic<int64_t> dec_ns{0}, enc_ns{0};
+    double h2d_ms = 0, k_ms = 0, d2h_ms = 0;
+
+    // region descriptors of a host row buffer (C order, in_cz planes)
+    std::vector<int64_t> in_row_shape(in.shape);
+    in_row_shape[0] = in_cz;
+    const std::vector<int64_t> in_row_st = c_strides(in_row_shape);
+    std::vector<int64_t> out_row_shape(out.shape);
+    out_row_shape[0] = out_cz;
+    const std::vector<int64_t> out_row_st = c_strides(out_row_shape);
+
+    auto submit_decode = [&](int64_t j) {
+        const int64_t s = j % NR;
+        if (ring_row[s] >= 0) {
+            dec_group[s].wait();
+            if (ring_ev_set[s]) HIPCHK(hipEventSynchronize(ring_ev[s]));  // H2D done reading it
+        }
+        ring_row[s] = j;
+        uint8_t* buf = hin[s].u8();
+        for (auto& idx : chunks_in_rows(in, j, j + 1)) {
+            pool.submit(dec_group[s], [&, idx, buf, j] {
+                const auto t0 = Clock::now();
+                std::vector<int64_t> origin(nd, 0);
+                origin[0] = j * in_cz;
+                size_t n = in.read_chunk(idx.data(), buf, origin.data(), in_row_shape.data(),
+                                         in_row_st.data());
+                bytes_read += n;
+                dec_ns += (int64_t)(secs_since(t0) * 1e9);
+            });
+        }
+    };
+    auto submit_encode = [&](int64_t k) {
+        const int s = (int)(k % 2);
+        uint8_t* buf = hout[s].u8();
+        for (auto& idx : chunks_in_rows(out, k, k + 1)) {
+            pool.submit(enc_group[s], [&, idx, buf, k] {
+                const auto t0 = Clock::now();
+                std::vector<int64_t> origin(out.ndim(), 0);
+                origin[0] = k * out_cz;
+                size_t n = out.write_chunk(idx.data(), buf, origin.data(), out_row_shape.data(),
+                                           out_row_st.data());
+                bytes_written += n;
+                enc_ns += (int64_t)(secs_since(t0) * 1e9);
+            });
+        }
+    };
+
+    int64_t next_dec;
+    {
+        int64_t a, b, j0, j1;
+        span(row_begin, a, b, j0, j1);
+        next_dec = j0;
+    }
+    const int64_t in_rows_total = (nz_in + in_cz - 1) / in_cz;
+    int64_t pending_enc = -1;  // output row whose D2H is queued but not yet handed to the encoders
+    auto finish_row = [&](int64_t k) {
+        const int s = (int)(k % 2);
+        HIPCHK(hipEventSynchronize(ev_d2h[s]));
+        h2d_ms += ev_ms(ev_h2d0[s], ev_h2d[s]);
+        k_ms += ev_ms(ev_k0[s], ev_k[s]);
+        d2h_ms += ev_ms(ev_d2h0[s], ev_d2h[s]);
+        submit_encode(k);
+    };
+    try {
+        for (int64_t k = row_begin; k < row_end; ++k) {
+            int64_t in0, in1, j0, j1;
+            span(k, in0, in1, j0, j1);
+            int64_t nj0 = j1 + 1, nj1 = j1 + 1;  // rows of the next output row (lookahead)
+            if (k + 1 < row_end) {
+                int64_t a, b;
+                span(k + 1, a, b, nj0, nj1);
+            }
+            const int64_t want = std::min(std::max(j1, nj1), in_rows_total - 1);
+            while (next_dec <= want && next_dec - NR < j0) submit_decode(next_dec++);
+            for (int64_t j = j0; j <= j1; ++j) dec_group[j % NR].wait();
+            const int s = (int)(k % 2);
+            enc_group[s].wait();  // host output buffer s is free again (row k-2 encoded)
+            // H2D: the slab's planes from the ring rows that hold them
+            HIPCHK(hipStreamWaitEvent(s_h2d, ev_k[s], 0));  // kernel k-2 no longer reads slab s
+            HIPCHK(hipEventRecord(ev_h2d0[s], s_h2d));
+            for (int64_t j = j0; j <= j1; ++j) {
+                const int64_t p0 = std::max(in0, j * in_cz), p1 = std::min(in1, (j + 1) * in_cz);
+                HIPCHK(hipMemcpyAsync(dslab[s].u8() + (size_t)(p0 - in0) * in_pb,
+                                      hin[j % NR].u8() + (size_t)(p0 - j * in_cz) * in_pb,
+                                      (size_t)(p1 - p0) * in_pb, hipMemcpyHostToDevice, s_h2d));
+            }
+            HIPCHK(hipEventRecord(ev_h2d[s], s_h2d));
+            for (int64_t j = j0; j <= j1; ++j) {
+                HIPCHK(hipEventRecord(ring_ev[j % NR], s_h2d));
+                ring_ev_set[j % NR] = true;
+            }
+            // kernel
+            HIPCHK(hipStreamWaitEvent(s_comp, ev_h2d[s], 0));
+            HIPCHK(hipStreamWaitEvent(s_comp, ev_d2h[s], 0));  // D2H k-2 done with dout[s]
+            HIPCHK(hipEventRecord(ev_k0[s], s_comp));
+            const int64_t z0 = k * out_cz, z1 = std::min(z0 + out_cz, nz_out);
+            if (int rc = op.apply(ctx.c, dslab[s].p, in0, in1, dout[s].p, z0, z1))
+                throw zt::zarr::Error(rc, zt_last_error());
+            HIPCHK(hipEventRecord(ev_k[s], s_comp));
+            // D2H
+            HIPCHK(hipStreamWaitEvent(s_d2h, ev_k[s], 0));
+            HIPCHK(hipEventRecord(ev_d2h0[s], s_d2h));
+            HIPCHK(hipMemcpyAsync(hout[s].u8(), dout[s].p, (size_t)(z1 - z0) * out_pb,
+                                  hipMemcpyDeviceToHost, s_d2h));
+            HIPCHK(hipEventRecord(ev_d2h[s], s_d2h));
+            if (pending_enc >= 0) finish_row(pending_enc);
+            pending_enc = k;
+        }
+        if (pending_enc >= 0) finish_row(pending_enc);
+        enc_group[0].wait();
+        enc_group[1].wait();
+        for (auto& g : dec_group) g.wait();
+    } catch (...) {
+        for (auto& g : dec_group) g.wait_nothrow();
+        enc_group[0].wait_nothrow();
+        enc_group[1].wait_nothrow();
+        (void)hipDeviceSynchronize();
+        throw;
+    }
+    if (st) {
+        st->wall_s = secs_since(t_start);
+        st->decode_s = dec_ns.load() * 1e-9;
+        st->encode_s = enc_ns.load() * 1e-9;
+        st->h2d_s = h2d_ms * 1e-3;
+        st->kernel_s = k_ms * 1e-3;
+        st->d2h_s = d2h_ms * 1e-3;
+        st->bytes_read = bytes_read.load();
+        st->bytes_written = bytes_written.load();
+        int64_t vox = 0;
+        for (int64_t k = row_begin; k < row_end; ++k)
+            vox += (std::min((k + 1) * out_cz, nz_out) - k * out_cz) * out_plane;
+        st->voxels = (uint64_t)vox;
+        st->rows = row_end - row_begin;
+        st->threads = pool.size();
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int zt_store_array_info(const char* path, int* dtype, int* ndim, int64_t* shape,
+                        int64_t* chunk_shape, int64_t* inner_chunk_shape) {
+    try {
+        if (!path) return zt::set_last_error(ZT_ERR_INVALID_PARAMETERS, "null path");
+        Array a = Array::open(path);
+        if (dtype) *dtype = a.dtype;
+        if (ndim) *ndim = a.ndim();
+        for (int d = 0; d < a.ndim() && d < ZT_MAX_DIMS; ++d) {
+            if (shape) shape[d] = a.shape[d];
+            if (chunk_shape) chunk_shape[d] = a.chunk_shape[d];
+            if (inner_chunk_shape)
+                inner_chunk_shape[d] = a.codecs.sharded ? a.codecs.inner_shape[d] : a.chunk_shape[d];
+        }
+        return ZT_OK;
+    } catch (const std::exception& e) {
+        return report(e);
+    }
+}
+
+int zt_store_create_array(const char* path, int dtype, int ndim, const int64_t* shape,
+                          const int64_t* chunk_shape, const char* codecs_json,
+                          const char* fill_value_json) {
+    try {
+        if (!path || !shape || !chunk_shape || ndim < 1 || ndim > ZT_MAX_DIMS)
+            return zt::set_last_error(ZT_ERR_INVALID_PARAMETERS, "bad array description");
+        zt::json::Value codecs = codecs_json ? zt::json::parse(codecs_json) : zt::json::Value();
+        zt::json::Value fill =
+            fill_value_json ? zt::json::parse(fill_value_json) : zt::json::Value((int64_t)0);
+        if (!fill_value_json && dtype == ZT_BOOL) fill = zt::json::Value(false);
+        if (!fill_value_json && dtype >= ZT_BFLOAT16) fill = zt::json::Value(0.0);
+        Array a = Array::create(path, dtype, std::vector<int64_t>(shape, shape + ndim),
+                                std::vector<int64_t>(chunk_shape, chunk_shape + ndim), codecs,
+                                fill);
+        a.store_metadata();
+        return ZT_OK;
+    } catch (const std::exception& e) {
+        return report(e);
+    }
+}
+
+int zt_store_read_subset(const char* path, const int64_t* start, const int64_t* shape,
+                         void* host_out, int nthreads) {
+    try {
+        if (!path || !start || !shape || !host_out)
+            return zt::set_last_error(ZT_ERR_INVALID_PARAMETERS, "null argument");
+        Array a = Array::open(path);
+        const int nd = a.ndim();
+        std::vector<int64_t> st(start, start + nd), sh(shape, shape + nd);
+        for (int d = 0; d < nd; ++d)
+            if (st[d] < 0 || sh[d] < 0 || st[d] + sh[d] > a.shape[d])
+                return zt::set_last_error(ZT_ERR_INVALID_PARAMETERS, "subset outside the array");
+        const auto strides = c_strides(sh);
+        std::vector<int64_t> c0(nd), c1(nd);
+        int64_t n = 1;
+        for (int d = 0; d < nd; ++d) {
+            if (sh[d] == 0) return ZT_OK;
+            c0[d] = st[d] / a.chunk_shape[d];
+            c1[d] = (st[d] + sh[d] - 1) / a.chunk_shape[d] + 1;
+            n *= c1[d] - c0[d];
+        }
+        Pool pool(resolve_threads(nthreads));
+        Group g;
+        uint8_t* dst = static_cast<uint8_t*>(host_out);
+        for (int64_t c = 0; c < n; ++c) {
+            std::vector<int64_t> idx(nd);
+            int64_t rem = c;
+            for (int d = nd - 1; d >= 0; --d) {
+                idx[d] = c0[d] + rem % (c1[d] - c0[d]);
+                rem /= c1[d] - c0[d];
+            }
+            pool.submit(g, [&, idx] { a.read_chunk(idx.data(), dst, st.data(), sh.data(), strides.data()); });
+        }
+        g.wait();
+        return ZT_OK;
+    } catch (const std::exception& e) {
+        return report(e);
+    }
+}
+
+int zt_store_write_subset(const char* path, const int64_t* start, const int64_t* shape,
+                          const void* host_in, int nthreads) {
+    try {
+        if (!path || !start || !shape || !host_in)
+            return zt::set_last_error(ZT_ERR_INVALID_PARAMETERS, "null argument");
+        Array a = Array::open(path);
+        const int nd = a.ndim();
+        std::vector<int64_t> st(start, start + nd), sh(shape, shape + nd);
+        std::vector<int64_t> c0(nd), c1(nd);
+        int64_t n = 1;
+        for (int d = 0; d < nd; ++d) {
+            if (st[d] < 0 || sh[d] < 0 || st[d] + sh[d] > a.shape[d])
+                return zt::set_last_error(ZT_ERR_INVALID_PARAMETERS, "subset outside the array");
+            if (st[d] % a.chunk_shape[d] != 0 ||
+                ((st[d] + sh[d]) % a.chunk_shape[d] != 0 && st[d] + sh[d] != a.shape[d]))
+                return zt::set_last_error(ZT_ERR_INVALID_PARAMETERS,
+                                          "write subset must be chunk aligned");
+            if (sh[d] == 0) return ZT_OK;
+            c0[d] = st[d] / a.chunk_shape[d];
+            c1[d] = (st[d] + sh[d] - 1) / a.chunk_shape[d] + 1;
+            n *= c1[d] - c0[d];
+        }
+        const auto strides = c_strides(sh);
+        Pool pool(resolve_threads(nthreads));
+        Group g;
+        const uint8_t* src = static_cast<const uint8_t*>(host_in);
+        for (int64_t c = 0; c < n; ++c) {
+            std::vector<int64_t> idx(nd);
+            int64_t rem = c;
+            for (int d = nd - 1; d >= 0; --d) {
+                idx[d] = c0[d] + rem % (c1[d] - c0[d]);
+                rem /= c1[d] - c0[d];
+            }
+            pool.submit(g, [&, idx] { a.write_chunk(idx.data(), src, st.data(), sh.data(), strides.data()); });
+        }
+        g.wait();
+        return ZT_OK;
+    } catch (const std::exception& e) {
+        return report(e);
+    }
+}
+
+int zt_store_write_synth(const char* path, int kind, uint64_t seed, int nthreads) {
+    try {
+        if (!path) return zt::set_last_error(ZT_ERR_INVALID_PARAMETERS, "null path");
+        Array a = Array::open(path);
+        if ((kind == 0 && a.dtype != ZT_FLOAT32) || (kind == 1 && a.dtype != ZT_UINT16) ||
+            kind < 0 || kind > 1)
+            return zt::set_last_error(ZT_ERR_UNSUPPORTED_DATA_TYPE,
+                                      "synthetic kind 0 needs float32, kind 1 uint16");
+        const int nd = a.ndim();
+        const auto g = a.grid_shape();
+        int64_t n = 1;
+        for (auto x : g) n *= x;
+        const auto astr = c_strides(a.shape);
+        const int64_t nx = a.shape[nd - 1];
+        Pool pool(resolve_threads(nthreads));
+        Group grp;
+        for (int64_t c = 0; c < n; ++c) {
+            pool.submit(grp, [&, c] {
+                std::vector<int64_t> idx(nd), org(nd), box(nd);
+                int64_t rem = c;
+                for (int d = nd - 1; d >= 0; --d) { idx[d] = rem % g[d]; rem /= g[d]; }
+                int64_t cnt = 1;
+                for (int d = 0; d < nd; ++d) {
+                    org[d] = idx[d] * a.chunk_shape[d];
+                    box[d] = std::min(a.chunk_shape[d], a.shape[d] - org[d]);
+                    cnt *= box[d];
+                }
+                std::vector<uint8_t> buf((size_t)cnt * a.esz);
+                const auto bst = c_strides(box);
+                for (int64_t i = 0; i < cnt; ++i) {
+                    int64_t r = i, gl = 0, x = 0;
+                    for (int d = nd - 1; d >= 0; --d) {
+                        int64_t p = org[d] + r % box[d];
+                        r /= box[d];
+                        gl += p * astr[d];
+                        if (d == nd - 1) x = p;
+                    }
+                    const uint64_t h = splitmix64(seed ^ (uint64_t)gl);
+                    if (kind == 0) {
+                        // same rounding as the device generator: RN(100*U) then + 500 (one RN)
+                        const float U = (float)(h >> 40) * (1.0f / 16777216.0f);
+                        volatile float t = 100.0f * U;
+                        const float v = t + (x >= nx / 2 ? 500.0f : 0.0f);
+                        std::memcpy(&buf[(size_t)i * 4], &v, 4);
+                    } else {
+                        const uint16_t v = (uint16_t)(((h >> 40) * 65535ull) >> 24);
+                        std::memcpy(&buf[(size_t)i * 2], &v, 2);
+                    }
+                }
+                a.write_chunk(idx.data(), buf.data(), org.data(), box.data(), bst.data());
+            });
+        }
+        grp.wait();
+        return ZT_OK;
+    } catch (const std::exception& e) {
+        return report(e);
+    }
+}
+
+int zt_store_create_output_like(const char* in_path, const char* out_path, int dtype_out) {
+    try {
+        if (!in_path || !out_path) return zt::set_last_error(ZT_ERR_INVALID_PARAMETERS, "null path");
+        Array in = Array::open(in_path);
+        const int dt = dtype_out < 0 ? in.dtype : dtype_out;
+        Array out = Array::create(out_path, dt, in.shape, in.chunk_shape, in.codecs.to_json(),
+                                  dt == in.dtype ? in.fill_json : convert_fill(in, dt));
+        out.store_metadata();
+        return ZT_OK;
+    } catch (const std::exception& e) {
+        return report(e);
+    }
+}
+
+int zt_store_guided_filter(const char* in_path, const char* out_path, int dtype_out,
+                           float epsilon, int radius, int device, int64_t row_begin,
+                           int64_t row_end, int nthreads, int flags, zt_store_stats* stats) {
+    try {
+        if (!in_path || !out_path) return zt::set_last_error(ZT_ERR_INVALID_PARAMETERS, "null path");
+        if (radius < 0 || radius > 127)
+            return zt::set_last_error(ZT_ERR_INVALID_PARAMETERS, "radius must be in [0, 127]");
+        Array in = Array::open(in_path);
+        const int dt = dtype_out < 0 ? in.dtype : dtype_out;
+        if (int rc = zt_guided_filter_is_compatible(in.dtype, dt)) return rc;
+        // output_array_builder: same shape, chunking and codecs; data type (and converted fill
+        // value) from --data-type (filter_traits.rs:47-82, lib.rs:409-650)
+        Array out = Array::create(out_path, dt, in.shape, in.chunk_shape, in.codecs.to_json(),
+                                  dt == in.dtype ? in.fill_json : convert_fill(in, dt));
+        if (flags & ZT_STORE_ERASE_OUTPUT_METADATA) out.erase_metadata();  // "not finished" marker
+        const int nd = in.ndim();
+        const int64_t halo = (int64_t)((radius * 2) & 0xFF);  // u8 arithmetic (guided_filter.rs:92)
+        const int64_t nz = in.shape[0];
+        RowOp op;
+        op.input_planes = [&](int64_t z0, int64_t z1, int64_t& a, int64_t& b) {
+            a = std::max<int64_t>(0, z0 - halo);
+            b = std::min(nz, z1 + halo);
+        };
+        const std::vector<int64_t> shape = in.shape, chunk = in.chunk_shape;
+        const int din = in.dtype;
+        op.apply = [&](zt_ctx* c, const void* slab, int64_t in0, int64_t in1, void* o, int64_t z0,
+                       int64_t z1) -> int {
+            if (nd == 3 && radius <= 8)
+                return zt_guided_filter_apply_slab(c, din, slab, dt, o, shape.data(), in0,
+                                                   in1 - in0, z0, z1 - z0, chunk.data(), epsilon,
+                                                   radius);
+            // n-D: the slab is a block whose windows clamp exactly where the array's do (it
+            // carries the halo or reaches the edge), so apply_ndarray on it is the chunked result
+            std::vector<int64_t> bshape(shape), ostart(nd, 0), oshape(shape);
+            bshape[0] = in1 - in0;
+            ostart[0] = z0 - in0;
+            oshape[0] = z1 - z0;
+            return zt_guided_filter_apply_ndarray(c, din, slab, bshape.data(), nullptr, nd,
+                                                  ostart.data(), oshape.data(), dt, o, nullptr,
+                                                  epsilon, radius);
+        };
+        run_pipeline(in, out, device, row_begin, row_end, nthreads, op, stats);
+        if (flags & ZT_STORE_FINISH_OUTPUT) out.store_metadata();
+        return ZT_OK;
+    } catch (const std::exception& e) {
+        return report(e);
+    }
+}
+
+int zt_store_downsample(const char* in_path, const char* out_path, const int64_t* stride,
+                        int discrete, int dtype_out, int device, int64_t row_begin,
+                        int64_t row_end, int nthreads, int flags, zt_store_stats* stats) {
+    try {
+        if (!in_path || !out_path || !stride)
+            return zt::set_last_error(ZT_ERR_INVALID_PARAMETERS, "null argument");
+        Array in = Array::open(in_path);
+        const int nd = in.ndim();
+        const int dt = dtype_out < 0 ? in.dtype : dtype_out;
+        if (int rc = zt_downsample_is_compatible(in.dtype, dt, discrete)) return rc;
+        std::vector<int64_t> st(stride, stride + nd), oshape(nd), win(nd);
+        if (int rc = zt_downsample_output_shape(in.shape.data(), nd, st.data(), oshape.data()))
+            return rc;
+        for (int d = 0; d < nd; ++d) win[d] = std::min(st[d], in.shape[d]);
+        // zarrs_ome.rs:549-559: output chunk = min(input chunk, output shape) per axis
+        std::vector<int64_t> ochunk(nd);
+        for (int d = 0; d < nd; ++d) ochunk[d] = std::min(in.chunk_shape[d], oshape[d]);
+        zt::json::Value codecs = in.codecs.to_json();
+        if (in.codecs.sharded) {
+            // keep the inner chunk no larger than the (possibly shrunk) shard
+            Array probe = in;
+            for (int d = 0; d < nd; ++d)
+                probe.codecs.inner_shape[d] = std::min(in.codecs.inner_shape[d], ochunk[d]);
+            for (int d = 0; d < nd; ++d)
+                if (ochunk[d] % probe.codecs.inner_shape[d]) probe.codecs.inner_shape[d] = ochunk[d];
+            codecs = probe.codecs.to_json();
+        }
+        Array out = Array::create(out_path, dt, oshape, ochunk, codecs,
+                                  dt == in.dtype ? in.fill_json : convert_fill(in, dt));
+        if (flags & ZT_STORE_ERASE_OUTPUT_METADATA) out.erase_metadata();
+        const int din = in.dtype;
+        const int64_t w0 = win[0];
+        RowOp op;
+        op.input_planes = [&](int64_t z0, int64_t z1, int64_t& a, int64_t& b) {
+            a = z0 * w0;
+            b = std::min(z1 * w0, in.shape[0]);  // input_subset (downsample.rs:64-70)
+        };
+        const std::vector<int64_t> ishape = in.shape;
+        op.apply = [&](zt_ctx* c, const void* slab, int64_t in0, int64_t in1, void* o, int64_t z0,
+                       int64_t z1) -> int {
+            std::vector<int64_t> bshape(ishape);
+            bshape[0] = in1 - in0;
+            return zt_downsample_apply_ndarray(c, din, slab, bshape.data(), nd, st.data(),
+                                               discrete, dt, o);
+        };
+        run_pipeline(in, out, device, row_begin, row_end, nthreads, op, stats);
+        if (flags & ZT_STORE_FINISH_OUTPUT) out.store_metadata();
+        return ZT_OK;
+    } catch (const std::exception& e) {
+        return report(e);
+    }
+}
+
+int zt_store_codec_available(const char* name) {
+    if (!name) return 0;
+    std::string n(name);
+    if (n == "bytes" || n == "gzip" || n == "crc32c" || n == "sharding_indexed") return 1;
+    if (n == "zstd") return zt::zarr::zstd_available() ? 1 : 0;
+    return 0;
+}
+
+}  // extern "C"

@@ -174,6 +174,8 @@ int run_fused3(zt_ctx* ctx, int dtype_in, const void* in, const int64_t dom[3], 
     p.out_sz = out_sz;
     p.out_sy = out_sy;
     p.in_z0 = (int)in_z0;
+    p.zlo = (int)std::max<int64_t>(0, in_z0);
+    p.zhi = (int)std::min<int64_t>(dom[0], in_z0 + in_rows);
     p.nz = (int)dom[0];
     p.ny = (int)dom[1];
     p.nx = (int)dom[2];
@@ -254,6 +256,14 @@ int run_separable(zt_ctx* ctx, int dtype_in, const void* in, const int64_t* shap
 }
 
 }  // namespace
+
+namespace zt {
+// Used by the host store / pipeline code (host/*.cpp) to report errors through zt_last_error().
+int set_last_error(int code, const char* msg) {
+    g_last_error = msg ? msg : "";
+    return code;
+}
+}  // namespace zt
 
 extern "C" {
 

@@ -21,6 +21,7 @@ struct GFParams {
     int64_t in_sz, in_sy;
     int64_t out_sz, out_sy;
     int in_z0;
+    int zlo, zhi;  // input planes present in `in`: [zlo, zhi) = [in_z0, in_z0 + rows) within [0, nz)
     int nz, ny, nx;
     int oz0, oy0, ox0;
     int onz, ony, onx;

@@ -1,0 +1,164 @@
+"""Zarr V3 filesystem arrays and the store -> store filters (host side of the C ABI).
+
+Mirrors what the reference does through zarrs (0.20.0-beta.2): ``load_array`` / ``create_array``
+in src/bin/zarrs_filter.rs:63-87, the filters' ``apply`` over Array<FilesystemStore>
+(guided_filter.rs:240-319, downsample.rs:170-286) and zarrs_ome's level loop
+(zarrs_ome.rs:515-738). All I/O and compute run in libzarrs_tools_amd.so; this module only
+marshals arguments (numpy is used for host buffers in tests and tools).
+"""
+from __future__ import annotations
+
+import ctypes
+import json
+import os
+from dataclasses import dataclass
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import _abi
+from ._abi import DTYPES, DTYPE_NAMES, check, i64_array, lib
+
+NUMPY = {
+    "bool": np.bool_, "int8": np.int8, "int16": np.int16, "int32": np.int32, "int64": np.int64,
+    "uint8": np.uint8, "uint16": np.uint16, "uint32": np.uint32, "uint64": np.uint64,
+    "bfloat16": np.uint16, "float16": np.float16, "float32": np.float32, "float64": np.float64,
+}
+
+SYNTH_STEP_NOISE_F32 = 0
+SYNTH_U16 = 1
+SEED = 0x5EED2025
+
+
+def _b(path) -> bytes:
+    return os.fspath(path).encode()
+
+
+def _dt(dtype) -> int:
+    if dtype is None:
+        return -1
+    if isinstance(dtype, int):
+        return dtype
+    if dtype not in DTYPES:
+        raise _abi.UnsupportedDataType(_abi.ERR_UNSUPPORTED_DATA_TYPE,
+                                       f"unsupported data type {dtype}")
+    return DTYPES[dtype]
+
+
+@dataclass
+class ArrayInfo:
+    path: str
+    data_type: str
+    shape: tuple
+    chunk_shape: tuple
+    inner_chunk_shape: tuple
+
+    @property
+    def ndim(self) -> int:
+        return len(self.shape)
+
+    @property
+    def metadata(self) -> dict:
+        with open(os.path.join(self.path, "zarr.json")) as f:
+            return json.load(f)
+
+
+def open_array(path) -> ArrayInfo:
+    """Array::open on a filesystem store (zarr.json V3)."""
+    dt, nd = ctypes.c_int(), ctypes.c_int()
+    shp, ch, inner = (ctypes.c_int64 * 8)(), (ctypes.c_int64 * 8)(), (ctypes.c_int64 * 8)()
+    check(lib().zt_store_array_info(_b(path), ctypes.byref(dt), ctypes.byref(nd), shp, ch, inner))
+    n = nd.value
+    return ArrayInfo(os.fspath(path), DTYPE_NAMES[dt.value], tuple(shp[:n]), tuple(ch[:n]),
+                     tuple(inner[:n]))
+
+
+def codecs_json(compression: Optional[str] = None, level: int = 1,
+                shard_inner: Optional[Sequence[int]] = None) -> Optional[str]:
+    """A Zarr V3 codec list: bytes (+ gzip/zstd), optionally inside sharding_indexed."""
+    chain = [{"name": "bytes", "configuration": {"endian": "little"}}]
+    if compression == "gzip":
+        chain.append({"name": "gzip", "configuration": {"level": int(level)}})
+    elif compression == "zstd":
+        chain.append({"name": "zstd", "configuration": {"level": int(level), "checksum": False}})
+    elif compression not in (None, "none"):
+        raise ValueError(f"unknown compression {compression}")
+    if shard_inner is not None:
+        chain = [{"name": "sharding_indexed", "configuration": {
+            "chunk_shape": [int(c) for c in shard_inner], "codecs": chain,
+            "index_codecs": [{"name": "bytes", "configuration": {"endian": "little"}},
+                             {"name": "crc32c"}],
+            "index_location": "end"}}]
+    return json.dumps(chain)
+
+
+def create_array(path, data_type: str, shape, chunk_shape, codecs: Optional[str] = None,
+                 fill_value=None) -> ArrayInfo:
+    """ArrayBuilder::build + store_metadata for a filesystem store."""
+    shape = [int(s) for s in shape]
+    fv = None if fill_value is None else json.dumps(fill_value).encode()
+    check(lib().zt_store_create_array(_b(path), _dt(data_type), len(shape), i64_array(shape),
+                                      i64_array(chunk_shape),
+                                      None if codecs is None else codecs.encode(), fv))
+    return open_array(path)
+
+
+def read_array(path, start=None, shape=None, nthreads: int = 0) -> np.ndarray:
+    """Array::retrieve_array_subset_ndarray into a numpy array (bfloat16 as raw uint16)."""
+    info = open_array(path)
+    start = [0] * info.ndim if start is None else [int(s) for s in start]
+    shape = list(info.shape) if shape is None else [int(s) for s in shape]
+    out = np.empty(shape, dtype=NUMPY[info.data_type])
+    check(lib().zt_store_read_subset(_b(path), i64_array(start), i64_array(shape),
+                                     out.ctypes.data_as(ctypes.c_void_p), int(nthreads)))
+    return out
+
+
+def write_array(path, data: np.ndarray, start=None, nthreads: int = 0) -> None:
+    """Array::store_array_subset_ndarray for a chunk-aligned subset."""
+    info = open_array(path)
+    data = np.ascontiguousarray(data)
+    start = [0] * info.ndim if start is None else [int(s) for s in start]
+    check(lib().zt_store_write_subset(_b(path), i64_array(start), i64_array(data.shape),
+                                      data.ctypes.data_as(ctypes.c_void_p), int(nthreads)))
+
+
+def write_synth(path, kind: int = SYNTH_STEP_NOISE_F32, seed: int = SEED,
+                nthreads: int = 0) -> None:
+    """Fill an array with the SURVEY.md §8(d) synthetic volume (same values as the device
+    generator and oracle.synth_step_noise_f32 / synth_u16)."""
+    check(lib().zt_store_write_synth(_b(path), int(kind), int(seed), int(nthreads)))
+
+
+def codec_available(name: str) -> bool:
+    return bool(lib().zt_store_codec_available(name.encode()))
+
+
+def _flags(erase: bool, finish: bool) -> int:
+    return (_abi.STORE_ERASE_OUTPUT_METADATA if erase else 0) | (
+        _abi.STORE_FINISH_OUTPUT if finish else 0)
+
+
+def guided_filter(input_path, output_path, epsilon: float, radius: int,
+                  data_type: Optional[str] = None, device: int = 0, rows=None,
+                  nthreads: int = 0, erase: bool = True, finish: bool = True) -> dict:
+    """zarrs_filter guided-filter INPUT OUTPUT EPSILON RADIUS [--data-type T] on GPU `device`.
+    `rows` = (begin, end) output chunk rows along axis 0 (None = all). Returns the run stats."""
+    st = _abi.StoreStats()
+    r0, r1 = (0, -1) if rows is None else (int(rows[0]), int(rows[1]))
+    check(lib().zt_store_guided_filter(_b(input_path), _b(output_path), _dt(data_type),
+                                       float(epsilon), int(radius), int(device), r0, r1,
+                                       int(nthreads), _flags(erase, finish), ctypes.byref(st)))
+    return st.as_dict()
+
+
+def downsample(input_path, output_path, stride, discrete: bool = False,
+               data_type: Optional[str] = None, device: int = 0, rows=None, nthreads: int = 0,
+               erase: bool = True, finish: bool = True) -> dict:
+    """zarrs_filter downsample INPUT OUTPUT STRIDE [--discrete] / one zarrs_ome level."""
+    st = _abi.StoreStats()
+    r0, r1 = (0, -1) if rows is None else (int(rows[0]), int(rows[1]))
+    check(lib().zt_store_downsample(_b(input_path), _b(output_path), i64_array(stride),
+                                    int(bool(discrete)), _dt(data_type), int(device), r0, r1,
+                                    int(nthreads), _flags(erase, finish), ctypes.byref(st)))
+    return st.as_dict()
