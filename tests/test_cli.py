@@ -1,0 +1,62 @@
+"""CPU: the zarrs_filter / zarrs_ome command-line surface (argument grammar, run configs, error
+behaviour) without device work. The GPU runs of the same commands are in test_cli_gpu.py."""
+import json
+
+import numpy as np
+import pytest
+
+from zarrs_tools_amd import _abi
+from zarrs_tools_amd import store as S
+from zarrs_tools_amd import zarrs_filter as ZF
+from zarrs_tools_amd import zarrs_ome as ZO
+
+
+def test_guided_filter_subcommand_grammar():
+    # zarrs_filter guided-filter IN OUT EPSILON RADIUS [--data-type T] (guided_filter.rs:25-33)
+    a = ZF.build_parser().parse_args(["guided-filter", "in.zarr", "out.zarr", "40000", "3",
+                                      "--data-type", "float32"])
+    steps = ZF._steps_from_cli(a)
+    assert steps == [{"filter": "guided_filter", "input": "in.zarr", "output": "out.zarr",
+                      "epsilon": 40000.0, "radius": 3, "data_type": "float32",
+                      "chunk_limit": None}]
+
+
+def test_downsample_subcommand_grammar():
+    a = ZF.build_parser().parse_args(["downsample", "i", "o", "2,2,1", "--discrete"])
+    assert ZF._steps_from_cli(a)[0]["stride"] == [2, 2, 1]
+    assert ZF._steps_from_cli(a)[0]["discrete"] is True
+
+
+def test_off_path_filter_is_rejected(tmp_path):
+    S.create_array(tmp_path / "in", "uint8", (4,), (4,))
+    with pytest.raises(_abi.FilterError, match="outside the accelerated path"):
+        ZF.run([{"filter": "gaussian", "input": str(tmp_path / "in"), "output": "x"}],
+               log=lambda *a: None)
+
+
+def test_first_filter_needs_input():
+    with pytest.raises(_abi.InvalidParameters):
+        ZF.run([{"filter": "guided_filter", "epsilon": 1.0, "radius": 1}], log=lambda *a: None)
+
+
+def test_exists_exit_refuses_existing_output(tmp_path):
+    S.create_array(tmp_path / "in", "float32", (4, 4), (2, 2))
+    S.create_array(tmp_path / "out", "float32", (4, 4), (2, 2))
+    with pytest.raises(_abi.FilterError, match="already exists"):
+        ZF.run([{"filter": "guided_filter", "input": str(tmp_path / "in"),
+                 "output": str(tmp_path / "out"), "epsilon": 1.0, "radius": 1}], exists="exit",
+               log=lambda *a: None)
+
+
+def test_run_config_file_and_missing_args(tmp_path):
+    S.create_array(tmp_path / "in", "float32", (4, 4), (2, 2))
+    cfg = tmp_path / "run.json"
+    cfg.write_text(json.dumps([{"filter": "guided_filter", "input": str(tmp_path / "in"),
+                                "output": "$tmp"}]))
+    assert ZF.main([str(cfg)]) == 1  # no epsilon / radius -> InvalidParameters, exit code 1
+
+
+def test_ome_factor_rank_mismatch(tmp_path):
+    S.create_array(tmp_path / "in", "uint16", (8, 8), (4, 4))
+    with pytest.raises(_abi.InvalidParameters):
+        ZO.run(str(tmp_path / "in"), str(tmp_path / "out"), factor=[2, 2, 2], log=lambda *a: None)

@@ -7,6 +7,7 @@
 #include <fcntl.h>
 #include <sys/stat.h>
 #include <sys/types.h>
+#include <sys/uio.h>
 #include <unistd.h>
 #include <zlib.h>
 
@@ -157,6 +158,70 @@ std::vector<int64_t> to_ints(const json::Value& v) {
     std::vector<int64_t> out;
     for (auto& e : v.arr()) out.push_back(e.as_int());
     return out;
+}
+
+
+// Scatter a file's byte runs into memory (or gather memory runs into a file) with preadv /
+// pwritev: the uncompressed `bytes` codec needs no staging copy between the chunk file and the
+// strided row buffer. Runs are (file offset, memory pointer, length); consecutive runs whose file
+// ranges touch are issued as one vectored call (<= IOV_MAX iovecs).
+struct Run {
+    int64_t off;
+    uint8_t* mem;
+    size_t len;
+};
+
+void vector_io(int fd, const std::vector<Run>& runs, bool write, const std::string& what) {
+    size_t i = 0;
+    std::vector<struct iovec> iov;
+    while (i < runs.size()) {
+        iov.clear();
+        const int64_t start = runs[i].off;
+        int64_t end = start;
+        size_t total = 0;
+        while (i < runs.size() && runs[i].off == end && iov.size() < 1024) {
+            iov.push_back({runs[i].mem, runs[i].len});
+            end += (int64_t)runs[i].len;
+            total += runs[i].len;
+            ++i;
+        }
+        size_t done = 0;
+        size_t k = 0;
+        while (done < total) {
+            ssize_t n = write ? ::pwritev(fd, iov.data() + k, (int)(iov.size() - k), start + (int64_t)done)
+                              : ::preadv(fd, iov.data() + k, (int)(iov.size() - k), start + (int64_t)done);
+            if (n <= 0) raise(ZT_ERR_IO, (write ? "write " : "read ") + what + ": " + std::strerror(errno));
+            done += (size_t)n;
+            // advance over the consumed iovecs
+            size_t m = (size_t)n;
+            while (m > 0 && k < iov.size()) {
+                if (m >= iov[k].iov_len) { m -= iov[k].iov_len; ++k; }
+                else {
+                    iov[k].iov_base = static_cast<uint8_t*>(iov[k].iov_base) + m;
+                    iov[k].iov_len -= m;
+                    m = 0;
+                }
+            }
+        }
+    }
+}
+
+// The runs of an n-D box: for every index of the outer axes, the innermost contiguous run.
+void box_runs(const int64_t* box, int nd, const int64_t* file_st, int64_t file_off,
+              uint8_t* mem, const int64_t* mem_st, size_t esz, std::vector<Run>& out) {
+    int64_t outer = 1;
+    for (int d = 0; d < nd - 1; ++d) outer *= box[d];
+    out.reserve((size_t)outer);
+    for (int64_t o = 0; o < outer; ++o) {
+        int64_t rem = o, fo = 0, mo = 0;
+        for (int d = nd - 2; d >= 0; --d) {
+            int64_t i = rem % box[d];
+            rem /= box[d];
+            fo += i * file_st[d];
+            mo += i * mem_st[d];
+        }
+        out.push_back({(file_off + fo) * (int64_t)esz, mem + mo * (int64_t)esz, (size_t)box[nd - 1] * esz});
+    }
 }
 
 }  // namespace
@@ -709,8 +774,34 @@ size_t Array::read_chunk(const int64_t* idx, uint8_t* dst, const int64_t* dst_or
         doff += (lo[d] - dst_origin[d]) * dst_strides[d];
         soff += (lo[d] - idx[d] * chunk_shape[d]) * cst[d];
     }
+    const bool raw_codec = !codecs.sharded && codecs.b2b.empty() && !codecs.big_endian;
+    if (raw_codec && dst_strides[nd - 1] == 1) {
+        // uncompressed: scatter the needed runs of the file straight into the destination
+        const std::string p = chunk_path(idx);
+        int fd = ::open(p.c_str(), O_RDONLY);
+        if (fd >= 0) {
+            struct stat stt;
+            if (fstat(fd, &stt) != 0 || (size_t)stt.st_size != (size_t)chunk_elems() * esz) {
+                ::close(fd);
+                raise(ZT_ERR_ARRAY, p + ": chunk has the wrong size");
+            }
+            std::vector<Run> runs;
+            box_runs(box.data(), nd, cst.data(), soff, dst + doff * esz, dst_strides, esz, runs);
+            try {
+                vector_io(fd, runs, false, p);
+            } catch (...) {
+                ::close(fd);
+                throw;
+            }
+            ::close(fd);
+            int64_t n = 1;
+            for (int d = 0; d < nd; ++d) n *= box[d];
+            return (size_t)n * esz;
+        }
+        if (errno != ENOENT) raise(ZT_ERR_IO, "open " + p + ": " + std::strerror(errno));
+    }
     bool exists = false;
-    std::string enc = read_file(chunk_path(idx), &exists);
+    std::string enc = raw_codec && dst_strides[nd - 1] == 1 ? std::string() : read_file(chunk_path(idx), &exists);
     if (!exists) {
         // missing chunk: the fill value over the region
         std::vector<int64_t> zero(nd, 0);
@@ -759,6 +850,26 @@ size_t Array::write_chunk(const int64_t* idx, const uint8_t* src, const int64_t*
     c_strides(chunk_shape, cst.data());
     int64_t soff = 0;
     for (int d = 0; d < nd; ++d) soff += (lo[d] - src_origin[d]) * src_strides[d];
+    const bool raw_codec = !codecs.sharded && codecs.b2b.empty() && !codecs.big_endian;
+    if (raw_codec && full && src_strides[nd - 1] == 1) {
+        // uncompressed full chunk: gather the runs of the source straight into the file
+        const std::string p = chunk_path(idx);
+        size_t slash = p.rfind('/');
+        if (slash != std::string::npos) mkdirs(p.substr(0, slash));
+        int fd = ::open(p.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+        if (fd < 0) raise(ZT_ERR_IO, "create " + p + ": " + std::strerror(errno));
+        std::vector<Run> runs;
+        box_runs(box.data(), nd, cst.data(), 0, const_cast<uint8_t*>(src) + soff * esz, src_strides,
+                 esz, runs);
+        try {
+            vector_io(fd, runs, true, p);
+        } catch (...) {
+            ::close(fd);
+            throw;
+        }
+        ::close(fd);
+        return (size_t)chunk_elems() * esz;
+    }
     std::vector<uint8_t> raw((size_t)chunk_elems() * esz);
     if (!full) fill_elems(raw.data(), (size_t)chunk_elems(), fill.data(), esz);
     copy_box(src + soff * esz, src_strides, raw.data(), cst.data(), box.data(), nd, esz);

@@ -1,0 +1,185 @@
+"""``zarrs_filter`` for the on-path filters: guided_filter and downsample over Zarr V3 stores.
+
+Mirrors src/bin/zarrs_filter.rs (LDeakin/zarrs_tools 0.7.2) for the filters this framework
+accelerates:
+
+    python -m zarrs_tools_amd.zarrs_filter [--exists erase|exit] [--tmp DIR] [--chunk-limit N]
+        [--device D] [RUN_CONFIG.json] [guided-filter IN OUT EPSILON RADIUS [--data-type T]
+                                        | downsample IN OUT STRIDE [--discrete] [--data-type T]]
+
+* subcommand arguments as GuidedFilterArguments (guided_filter.rs:25-33) and
+  DownsampleArguments (downsample.rs:20-33, STRIDE comma delimited);
+* a JSON run config is a list of {"filter": "guided_filter" | "downsample", "input", "output",
+  ...args, "data_type"}, with "$name" meaning a named temporary array under --tmp and an omitted
+  input meaning the previous filter's output (zarrs_filter.rs:106-138, :338-381);
+* `--exists erase` (default) overwrites an existing output, `exit` refuses it (:228-235);
+* the output metadata is erased before a filter runs and written when it finishes (:297-313).
+
+Filters outside the accelerated path (reencode, crop, rescale, clamp, equal, replace_value,
+gradient_magnitude, gaussian) are rejected with FilterError::Other: they are out of scope
+(DESIGN.md §1). `--chunk-limit` sets the number of host worker threads that decode and encode
+chunks (the reference's bound on concurrently processed chunks).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import shutil
+import sys
+import tempfile
+import time
+
+from . import _abi
+from . import store as S
+
+ON_PATH = ("guided_filter", "downsample")
+
+
+def _parse_stride(s: str):
+    return [int(x) for x in s.split(",") if x.strip()]
+
+
+def build_parser() -> argparse.ArgumentParser:
+    ap = argparse.ArgumentParser(prog="zarrs_filter",
+                                 description="Apply filters to a Zarr V3 array on an MI355X.")
+    ap.add_argument("--exists", choices=["erase", "exit"], default="erase")
+    ap.add_argument("--tmp", default=None, help="directory for temporary ($name) arrays")
+    ap.add_argument("--chunk-limit", type=int, default=None)
+    ap.add_argument("--device", type=int, default=0)
+    ap.add_argument("--stats", action="store_true", help="print per-filter stats as JSON")
+    sub = ap.add_subparsers(dest="filter")
+    g = sub.add_parser("guided-filter", help="Apply a guided filter (edge preserving noise filter).")
+    g.add_argument("input")
+    g.add_argument("output")
+    g.add_argument("epsilon", type=float)
+    g.add_argument("radius", type=int)
+    g.add_argument("--data-type", default=None)
+    g.add_argument("--chunk-limit", dest="filter_chunk_limit", type=int, default=None)
+    d = sub.add_parser("downsample", help="Downsample an image given a stride.")
+    d.add_argument("input")
+    d.add_argument("output")
+    d.add_argument("stride", type=_parse_stride)
+    d.add_argument("--discrete", action="store_true")
+    d.add_argument("--data-type", default=None)
+    d.add_argument("--chunk-limit", dest="filter_chunk_limit", type=int, default=None)
+    return ap
+
+
+def _steps_from_cli(a) -> list:
+    if a.filter == "guided-filter":
+        return [{"filter": "guided_filter", "input": a.input, "output": a.output,
+                 "epsilon": a.epsilon, "radius": a.radius, "data_type": a.data_type,
+                 "chunk_limit": a.filter_chunk_limit}]
+    if a.filter == "downsample":
+        return [{"filter": "downsample", "input": a.input, "output": a.output,
+                 "stride": a.stride, "discrete": a.discrete, "data_type": a.data_type,
+                 "chunk_limit": a.filter_chunk_limit}]
+    return []
+
+
+def run(steps: list, exists: str = "erase", tmp: str | None = None,
+        chunk_limit: int | None = None, device: int = 0, stats: bool = False,
+        log=print) -> list:
+    """Run a list of filter steps (the run-config form); returns the per-step stats."""
+    tmp_root = tmp or tempfile.gettempdir()
+    temps: dict[str, str] = {}
+    made: list[str] = []
+    last_output = None
+    results = []
+
+    def resolve(p, what):
+        if p is None:
+            if what == "input" and last_output is not None:
+                return last_output
+            if what == "output":
+                d = tempfile.mkdtemp(prefix="zt_", dir=tmp_root)
+                made.append(d)
+                return d
+            raise _abi.InvalidParameters(_abi.ERR_INVALID_PARAMETERS,
+                                         "the first filter needs an input")
+        if isinstance(p, str) and p.startswith("$"):
+            if p not in temps:
+                temps[p] = tempfile.mkdtemp(prefix=p[1:] + "_", dir=tmp_root)
+                made.append(temps[p])
+            return temps[p]
+        return p
+
+    t_all = time.perf_counter()
+    try:
+        for i, step in enumerate(steps):
+            name = step.get("filter")
+            if name not in ON_PATH:
+                raise _abi.FilterError(_abi.ERR_OTHER,
+                                       f"filter {name!r} is outside the accelerated path "
+                                       f"(supported: {', '.join(ON_PATH)})")
+            src = resolve(step.get("input"), "input")
+            dst = resolve(step.get("output"), "output")
+            if exists == "exit" and os.path.exists(os.path.join(dst, "zarr.json")):
+                raise _abi.FilterError(_abi.ERR_OTHER, f"output {dst} already exists")
+            if os.path.isdir(dst) and not dst.startswith(tmp_root):
+                shutil.rmtree(dst)  # create_array erases the output prefix (zarrs_filter.rs:76)
+            threads = step.get("chunk_limit") or chunk_limit or 0
+            info = S.open_array(src)
+            if name == "guided_filter":
+                if "epsilon" not in step or "radius" not in step:
+                    raise _abi.InvalidParameters(_abi.ERR_INVALID_PARAMETERS,
+                                                 "guided_filter needs epsilon and radius")
+                log(f"{i}: guided_filter epsilon={step['epsilon']} radius={step['radius']} "
+                    f"{src} ({info.data_type} {list(info.shape)}) -> {dst}")
+                st = S.guided_filter(src, dst, float(step["epsilon"]), int(step["radius"]),
+                                     data_type=step.get("data_type"), device=device,
+                                     nthreads=threads)
+            else:
+                stride = step.get("stride")
+                if isinstance(stride, str):
+                    stride = _parse_stride(stride)
+                if not stride or len(stride) != info.ndim:
+                    raise _abi.InvalidParameters(_abi.ERR_INVALID_PARAMETERS,
+                                                 "downsample stride must match the array rank")
+                log(f"{i}: downsample stride={stride} discrete={bool(step.get('discrete'))} "
+                    f"{src} ({info.data_type} {list(info.shape)}) -> {dst}")
+                st = S.downsample(src, dst, stride, discrete=bool(step.get("discrete", False)),
+                                  data_type=step.get("data_type"), device=device,
+                                  nthreads=threads)
+            out = S.open_array(dst)
+            log(f"   -> {out.data_type} {list(out.shape)} in {st['wall_s']:.2f}s "
+                f"(rw:{st['decode_s']:.2f}/{st['encode_s']:.2f} p:{st['kernel_s']:.3f})")
+            if stats:
+                log(json.dumps({"step": i, "filter": name, **st}))
+            results.append(st)
+            last_output = dst
+    finally:
+        for d in made:
+            shutil.rmtree(d, ignore_errors=True)
+    log(f"Completed in {time.perf_counter() - t_all:.2f}s")
+    return results
+
+
+def main(argv=None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
+    config = None
+    # a leading positional JSON run config (Cli::run_config), before any subcommand
+    if argv and argv[0].endswith(".json") and os.path.exists(argv[0]):
+        config = argv.pop(0)
+    a = build_parser().parse_args(argv)
+    if config:
+        with open(config) as f:
+            steps = json.load(f)
+        if isinstance(steps, dict):
+            steps = [steps]
+    else:
+        steps = _steps_from_cli(a)
+    if not steps:
+        build_parser().print_help()
+        return 2
+    try:
+        run(steps, a.exists, a.tmp, a.chunk_limit, a.device, a.stats)
+    except _abi.FilterError as e:
+        print(f"Error: {e}", file=sys.stderr)
+        return 1
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
