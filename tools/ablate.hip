@@ -45,8 +45,10 @@ int main(int argc, char** argv) {
     hipStream_t s; CK(hipStreamCreate(&s));
     const char* names[] = {"full", "no leave load (1)", "no Lc load (2)", "no v5 load (4)",
                            "no enter load (8)", "no loads (15)", "no barrier (16)",
-                           "no pointwise (32)"};
-    constexpr int NV = 8;
+                           "no pointwise (32)", "P5 1 LDS read (64)", "P4 1 LDS read (128)",
+                           "P3 1 LDS read (256)", "no stage1 DPP (512)", "1-read P3+P4+P5 (448)", "no P12 (1024)",
+                           "no P3 (2048)", "no P4 (4096)", "no P5 (8192)", "no P3,P4,P5", "nothing but loads/stores"};
+    constexpr int NV = 19;
     std::vector<std::vector<float>> t(NV);
     for (int round = 0; round < 3; ++round) {
         t[0].push_back(run<0>(p, s, 3));
@@ -57,6 +59,17 @@ int main(int argc, char** argv) {
         t[5].push_back(run<15>(p, s, 3));
         t[6].push_back(run<16>(p, s, 3));
         t[7].push_back(run<32>(p, s, 3));
+        t[8].push_back(run<64>(p, s, 3));
+        t[9].push_back(run<128>(p, s, 3));
+        t[10].push_back(run<256>(p, s, 3));
+        t[11].push_back(run<512>(p, s, 3));
+        t[12].push_back(run<448>(p, s, 3));
+        t[13].push_back(run<1024>(p, s, 3));
+        t[14].push_back(run<2048>(p, s, 3));
+        t[15].push_back(run<4096>(p, s, 3));
+        t[16].push_back(run<8192>(p, s, 3));
+        t[17].push_back(run<2048 + 4096 + 8192>(p, s, 3));
+        t[18].push_back(run<1024 + 2048 + 4096 + 8192>(p, s, 3));
     }
     for (int i = 0; i < NV; ++i) {
         std::sort(t[i].begin(), t[i].end());

@@ -12,6 +12,16 @@
 #include "zt_device.hpp"
 #include "zt_kernels.hpp"
 
+#ifndef GF_T3_TOP
+#define GF_T3_TOP 1
+#endif
+#ifndef GF_PRIO
+#define GF_PRIO 0
+#endif
+#ifndef GF_ORDER
+#define GF_ORDER 0
+#endif
+
 namespace zt {
 
 // ---------------------------------------------------------------------------------------------
@@ -434,7 +444,7 @@ struct GFConfig {
     static constexpr int OFF_DUMMY = OFF_RCP + SZ_RCP;  // 16-B sink for inactive lanes' writes
     static constexpr int LDS_BYTES = OFF_DUMMY + 256;
     // item -> thread placement: heavy phases on different waves (see C0 / C1)
-    static constexpr int T3 = NT - N3;  // P3 items on the top threads
+    static constexpr int T3 = GF_T3_TOP ? NT - N3 : 0;  // first thread of the P3 items
     static_assert(TX * TY % NT == 0, "tile must divide evenly over the threads");
     static_assert(TY % K5 == 0, "ring segment must divide the tile height");
     static_assert(TX % K4 == 0, "P4 segment must divide the tile width");
@@ -641,6 +651,7 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     // neighbours come from the adjacent lanes' quads by DPP wave shifts (whole rows per wave),
     // so the z-window never goes through LDS.
     auto do_p12 = [&](int tid) {
+        if constexpr (ABL & 1024) return;
 #pragma unroll
         for (int k = 0; k < C::NQP1; ++k) {
             int row, cq;
@@ -658,8 +669,13 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
             for (int n = 1; n <= NB; ++n)
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-                    win[4 * (NB - n) + e] = dpp_from_lower(win[4 * (NB - n + 1) + e]);
-                    win[4 * (NB + n) + e] = dpp_from_upper(win[4 * (NB + n - 1) + e]);
+                    if constexpr (ABL & 512) {
+                        win[4 * (NB - n) + e] = win[4 * (NB - n + 1) + e] * 0.5;
+                        win[4 * (NB + n) + e] = win[4 * (NB + n - 1) + e] * 0.25;
+                    } else {
+                        win[4 * (NB - n) + e] = dpp_from_lower(win[4 * (NB - n + 1) + e]);
+                        win[4 * (NB + n) + e] = dpp_from_upper(win[4 * (NB + n - 1) + e]);
+                    }
                 }
             double vin[4 + 2 * R], hs[4];
 #pragma unroll
@@ -720,11 +736,15 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     auto do_p3 = [&](int tid, int zc) {  // y-window (f64) of Hx -> U; a, b -> Lab
         const int item = tid - C::T3;
         if (item < 0) return;
+        if constexpr (ABL & 2048) return;
         const int col = item % C::E1X, sg = item / C::E1X;
         const double* src = Hx + (sg * C::K3) * C::PH + col;
         double vin[C::K3 + 2 * R], U[C::K3];
 #pragma unroll
-        for (int j = 0; j < C::K3 + 2 * R; ++j) vin[j] = src[j * C::PH];
+        for (int j = 0; j < C::K3 + 2 * R; ++j) {
+            if constexpr (ABL & 256) vin[j] = j == 0 ? src[0] : vin[j - 1] * 1.0001;
+            else vin[j] = src[j * C::PH];
+        }
         slide_sums_f64<R, C::K3>(vin, U);
         const float* vsrc = Lc + (sg * C::K3) * C::PC + C::XC + col;  // v of slice zc (C1)
         f2* lab = reinterpret_cast<f2*>(Lab);
@@ -774,12 +794,16 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     auto do_p4 = [&](int tid) {  // x-window sums of (a, b) rows -> Hab
         const int item = tid;
         if (item >= C::N4) return;
+        if constexpr (ABL & 4096) return;
         const int row = item % C::E1Y, sg = item / C::E1Y;
         const float4* src = reinterpret_cast<const float4*>(Lab + row * C::PA + sg * C::K4);
         f2 vin[C::K4 + 2 * R], vout[C::K4];
+        float4 f0 = src[0];
 #pragma unroll
         for (int j = 0; j < (C::K4 + 2 * R) / 2; ++j) {
-            const float4 f = src[j];
+            float4 f;
+            if constexpr (ABL & 128) { f = f0; f0.x *= 1.0001f; f0.y *= 0.999f; f0.z *= 1.001f; f0.w *= 0.9999f; }
+            else f = src[j];
             vin[2 * j] = (f2){f.x, f.y};
             vin[2 * j + 1] = (f2){f.z, f.w};
         }
@@ -800,11 +824,15 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     // position P of block B+1 is suffix_B(P+1) + prefix_{B+1}(P). ~3 packed adds per output
     // instead of an f64 running sum (10 ops).
     auto do_p5 = [&](int tid, int zc, auto slot_c) {  // y-window -> slice sums; z; out -> Lout
+        if constexpr (ABL & 8192) return;
         const int col5 = tid % TX, seg5 = tid / TX;
         const f2* src = reinterpret_cast<const f2*>(Hab) + (seg5 * K5) * C::PB + col5;
         f2 vin[K5 + 2 * R], s2[K5];
 #pragma unroll
-        for (int j = 0; j < K5 + 2 * R; ++j) vin[j] = src[j * C::PB];
+        for (int j = 0; j < K5 + 2 * R; ++j) {
+            if constexpr (ABL & 64) vin[j] = j == 0 ? src[0] : vin[j - 1] * (f2){1.0001f, 0.999f};
+            else vin[j] = src[j * C::PB];
+        }
         core_window_sums<R, K5>(vin, s2);
         constexpr int P = decltype(slot_c)::value;
         f2 AB[K5];
@@ -941,10 +969,36 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
             const int i = i0 + k;
             const int tid = threadIdx.x;
             const rsrc_t r_b = rs_in(ob, zb);
+            // tools/ instrumentation only (ABL & 16384): per-wave stamps of one workgroup
+            auto stamp = [&](int slot) {
+                if constexpr (ABL & 16384) {
+                    const int st = i - zc_begin - 64;
+                    if ((int)blockIdx.x == p.trace_block && st >= 0 && st < 18 &&
+                        (threadIdx.x & 63) == 0)
+                        p.trace[(st * 16 + threadIdx.x / 64) * 8 + slot] =
+                            __builtin_amdgcn_s_memtime();
+                }
+            };
+            stamp(0);
+            // Fair progress across the waves of a SIMD: the hardware issues oldest-first, which
+            // staggers the waves so the youngest runs its last phase alone, latency exposed. A
+            // wave drops its priority as it completes a phase, so laggards catch up.
+            if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(3);
             // C0: P3(i) + P5(i-1) (LDS and registers only)
-            do_p3(tid, i);
-            if (i > zc_begin) do_p5(tid, i - 1, std::integral_constant<int, (k + W - 1) % W>{});
+            if constexpr (GF_ORDER & 1) {
+                if (i > zc_begin) do_p5(tid, i - 1, std::integral_constant<int, (k + W - 1) % W>{});
+                if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(1);
+                do_p3(tid, i);
+            } else {
+                do_p3(tid, i);
+                if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(1);
+                stamp(4);
+                if (i > zc_begin) do_p5(tid, i - 1, std::integral_constant<int, (k + W - 1) % W>{});
+            }
+            stamp(1);
             lds_barrier_abl<ABL>();
+            stamp(2);
+            if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(3);
             // C1: staging (store out(i-1-R), Lc <- slice i+1, Lv5 <- slice i-R), the loads of
             // the next step, P12(i+1), P4(i). Every wait here is for a load issued a step ago.
             store_out(tid, make_rsrc(out_base + os,
@@ -953,9 +1007,15 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
             write_v5(tid);
             load_c(rs_in(ob + off_c, zb + R + 1));
             load_v5(r_b);
+            stamp(6);
+            if constexpr (GF_PRIO >= 2) __builtin_amdgcn_s_setprio(2);
+            if constexpr (GF_ORDER & 2) do_p4(tid);
             do_p12(tid);
             load_p1(rs_in(ob + off_a, zb + 2 * R + 1), r_b);
-            do_p4(tid);
+            if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(1);
+            stamp(5);
+            if constexpr (!(GF_ORDER & 2)) do_p4(tid);
+            stamp(3);
             lds_barrier_abl<ABL>();
             ++zb;
             ob += sstride;
@@ -1050,9 +1110,9 @@ inline bool fused_fast_dtype(int d) { return d == kF32 || d == kU16 || d == kU8 
         auto pick_out = [&](auto tin) -> hipError_t {                                             \
             using TI = decltype(tin);                                                             \
             switch (dout) {                                                                       \
-            case kF32: return launch_fused_cfg<R, TY, NT, TI, float>(p, s);                       \
-            case kU16: return launch_fused_cfg<R, TY, NT, TI, uint16_t>(p, s);                    \
-            case kU8: case kBool: return launch_fused_cfg<R, TY, NT, TI, uint8_t>(p, s);          \
+            case kF32: return launch_fused_auto<R, TY, NT, TI, float>(p, s);                      \
+            case kU16: return launch_fused_auto<R, TY, NT, TI, uint16_t>(p, s);                   \
+            case kU8: case kBool: return launch_fused_auto<R, TY, NT, TI, uint8_t>(p, s);         \
             default: return hipErrorInvalidValue;                                                 \
             }                                                                                     \
         };                                                                                        \

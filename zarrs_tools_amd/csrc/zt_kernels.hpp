@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
+
 namespace zt {
 
 constexpr int kMaxDims = 8;
@@ -30,6 +32,8 @@ struct GFParams {
     int itx0, itx1, ity0, ity1;  // interior tile range (fused kernel, host-computed)
     float eps;
     float rcp_w3;  // RN(1 / (2r+1)^3): the interior window count's reciprocal (host-computed)
+    unsigned long long* trace;  // tools/ only: s_memtime stamps of one workgroup (ABL & 16384)
+    int trace_block;
 };
 
 // N-d geometry for the separable path and downsample (C-order logical shapes).
@@ -45,6 +49,8 @@ struct NdGeom {
 };
 
 bool fused_supports_radius(int radius);
+// process-wide fused-kernel selection (zt_set_fused_variant): 0 default, 1 gf_v9.hpp
+std::atomic<int>& fused_variant();
 int fused_tile_y(int radius);  // output tile height of the fused kernel for this radius
 // element-type pairs with a direct fused instantiation; others are staged through f32
 bool fused_direct_pair(int dtype_in, int dtype_out);
