@@ -189,6 +189,31 @@ int zt_synth_u16(zt_ctx* ctx, uint16_t* out, const int64_t* shape, int ndim,
                  const int64_t* global_shape, int64_t z0, uint64_t seed);
 
 
+/* ---- Gaussian (src/filter/filters/gaussian.rs; src/filter/kernel.rs) ----------------------- */
+
+/* create_sampled_gaussian_kernel (gaussian.rs:252-267): writes the taps (2*half+1, or 1 when
+ * sigma == 0) to `taps` (may be NULL to query) and their count to *len. Host only. */
+int zt_gaussian_kernel(float sigma, int64_t kernel_half_size, float* taps, int64_t* len);
+/* Gaussian::is_compatible (gaussian.rs:123-147): all 13 types in and out. */
+int zt_gaussian_is_compatible(int dtype_in, int dtype_out);
+/* Gaussian::memory_per_chunk (gaussian.rs:149-168). */
+int zt_gaussian_memory_per_chunk(int dtype_in, int dtype_out, const int64_t* chunk_shape,
+                                 int ndim, const int64_t* kernel_half_size, uint64_t* bytes);
+/* Gaussian::apply_ndarray + extract_subset + `as` casts of apply_chunk (gaussian.rs:73-119,
+ * kernel.rs:17-73): the separable sampled Gaussian of a C-order device block (per axis, in axis
+ * order, f32 sequential tap sums, replicate edges at the block bounds), writing the region
+ * [out_start, out_start + out_shape) to `out` (C order, out_shape). sigma / kernel_half_size:
+ * ndim entries; kernel_half_size <= 127. Bit-identical to the reference. */
+int zt_gaussian_apply_ndarray(zt_ctx* ctx, int dtype_in, const void* in, const int64_t* in_shape,
+                              int ndim, const int64_t* out_start, const int64_t* out_shape,
+                              int dtype_out, void* out, const float* sigma,
+                              const int64_t* kernel_half_size);
+/* Gaussian::apply's chunk loop (gaussian.rs:170-249) over a device-resident C-order array: every
+ * chunk with its kernel_half_size halo, which equals one pass over the whole array. */
+int zt_gaussian_apply_array(zt_ctx* ctx, int dtype_in, const void* in, int dtype_out, void* out,
+                            const int64_t* shape, int ndim, const int64_t* chunk_shape,
+                            const float* sigma, const int64_t* kernel_half_size);
+
 /* ---- Zarr V3 store -> store path (host storage in and out) ----------------------------------
  * The reference's filters read and write Zarr arrays through zarrs (Array::retrieve_array_subset_
  * ndarray / store_array_subset_ndarray, guided_filter.rs:95-110; zarrs_ome.rs:226-232). These
@@ -251,6 +276,18 @@ int zt_store_guided_filter(const char* in_path, const char* out_path, int dtype_
 int zt_store_downsample(const char* in_path, const char* out_path, const int64_t* stride,
                         int discrete, int dtype_out, int device, int64_t row_begin,
                         int64_t row_end, int nthreads, int flags, zt_store_stats* stats);
+/* zarrs_filter gaussian IN OUT SIGMA HALF [--data-type T] over a store (Gaussian::apply,
+ * gaussian.rs:170-249): as zt_store_guided_filter, halo = kernel_half_size. */
+int zt_store_gaussian(const char* in_path, const char* out_path, int dtype_out, const float* sigma,
+                      const int64_t* kernel_half_size, int device, int64_t row_begin,
+                      int64_t row_end, int nthreads, int flags, zt_store_stats* stats);
+/* One zarrs_ome level with --gaussian-sigma (apply_chunk_continuous_gaussian, zarrs_ome.rs:
+ * 236-271): the Gaussian of each downsample input subset (plus its kernel_half_size halo), then
+ * the mean downsample of that f32 block to the level's data type. */
+int zt_store_downsample_gaussian(const char* in_path, const char* out_path, const int64_t* stride,
+                                 const float* sigma, const int64_t* kernel_half_size,
+                                 int dtype_out, int device, int64_t row_begin, int64_t row_end,
+                                 int nthreads, int flags, zt_store_stats* stats);
 /* 1 if the named codec can be read and written here, else 0. */
 int zt_store_codec_available(const char* name);
 

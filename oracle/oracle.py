@@ -75,6 +75,13 @@ def lib():
             i64p, i64p, i64p, ctypes.c_int, ctypes.c_float, ctypes.c_int, ctypes.c_int,
             ctypes.c_uint64, i64p]
         L.oracle_guided_filter_time_chunks.restype = ctypes.c_double
+        fp = ctypes.POINTER(ctypes.c_float)
+        L.oracle_gaussian_kernel.argtypes = [ctypes.c_float, ctypes.c_int64, fp]
+        L.oracle_gaussian_kernel.restype = ctypes.c_int64
+        L.oracle_gaussian_apply_ndarray.argtypes = [vp, i64p, ctypes.c_int, fp, i64p]
+        L.oracle_gaussian_apply_ndarray.restype = ctypes.c_int
+        L.oracle_gaussian_apply.argtypes = [vp, vp, i64p, ctypes.c_int, i64p, fp, i64p]
+        L.oracle_gaussian_apply.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -124,6 +131,39 @@ def guided_filter_apply_chunks(v: np.ndarray, out: np.ndarray, chunk_shape, epsi
     return lib().oracle_guided_filter_apply_chunks(
         _ptr(v), _ptr(out), _shape(v.shape), v.ndim, _shape(chunk_shape), float(epsilon),
         int(radius), int(nthreads), int(faithful), int(chunk_begin), int(chunk_end))
+
+
+def _floats(xs):
+    return (ctypes.c_float * len(xs))(*[float(x) for x in xs])
+
+
+def gaussian_kernel(sigma: float, half: int) -> np.ndarray:
+    """create_sampled_gaussian_kernel (gaussian.rs:252-267)."""
+    taps = (ctypes.c_float * (2 * int(half) + 1))()
+    n = lib().oracle_gaussian_kernel(float(sigma), int(half), taps)
+    return np.array(taps[:n], dtype=np.float32)
+
+
+def gaussian_apply_ndarray(v: np.ndarray, sigma, kernel_half_size) -> np.ndarray:
+    """Gaussian::apply_ndarray (gaussian.rs:110-119) on one whole block."""
+    out = np.array(v, dtype=np.float32, order="C", copy=True)
+    rc = lib().oracle_gaussian_apply_ndarray(_ptr(out), _shape(out.shape), out.ndim,
+                                             _floats(sigma), _shape(kernel_half_size))
+    if rc != 0:
+        raise ValueError(f"oracle_gaussian_apply_ndarray failed: {rc}")
+    return out
+
+
+def gaussian_apply(v: np.ndarray, chunk_shape, sigma, kernel_half_size) -> np.ndarray:
+    """Gaussian::apply (gaussian.rs:170-249): chunked, kernel_half_size halo per chunk."""
+    v = np.ascontiguousarray(v, dtype=np.float32)
+    out = np.empty_like(v)
+    rc = lib().oracle_gaussian_apply(_ptr(v), _ptr(out), _shape(v.shape), v.ndim,
+                                     _shape(chunk_shape), _floats(sigma),
+                                     _shape(kernel_half_size))
+    if rc != 0:
+        raise ValueError(f"oracle_gaussian_apply failed: {rc}")
+    return out
 
 
 def cast_from_f32(v: np.ndarray, dtype: str) -> np.ndarray:

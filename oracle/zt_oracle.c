@@ -712,3 +712,119 @@ double oracle_guided_filter_time_chunks(const int64_t* global_shape, const int64
     if (voxels_out) *voxels_out = vox;
     return t1 - t0;
 }
+
+/* ------------------------------------------------------------------------------------------ */
+/* Gaussian (gaussian.rs:110-119, :252-267; kernel.rs:17-73)                                   */
+/* ------------------------------------------------------------------------------------------ */
+
+/* gaussian.rs:252-267. Operation order as written there: t = sigma*sigma;
+ * scale = 1 / (2 * PI * t).sqrt(); tap(n) = scale * (-((n*n) as f32 / (2 * t))).exp(). f32::exp
+ * is the platform libm expf (glibc here, as for the reference on Linux). */
+int64_t oracle_gaussian_kernel(float sigma, int64_t half, float* taps) {
+    if (sigma == 0.0f) {
+        taps[0] = 1.0f;
+        return 1;
+    }
+    const float pi = 3.14159265358979323846f; /* std::f32::consts::PI */
+    const float t = sigma * sigma;
+    const float scale = 1.0f / sqrtf(2.0f * pi * t);
+    for (int64_t n = 0; n <= half; ++n) {
+        const float e = scale * expf(-((float)(uint64_t)(n * n) / (2.0f * t)));
+        taps[half - n] = e; /* reversed half, then the half without n = 0 */
+        taps[half + n] = e;
+    }
+    return 2 * half + 1;
+}
+
+/* kernel.rs:17-73 apply_1d_kernel along `axis` of a C-order block: out[k] = sum over the taps of
+ * in[min(k+i saturating_sub mid, n-1)] * tap[i], summed in tap order as f32 (Iterator::sum,
+ * no fused multiply-add). */
+static void gauss_1d(const float* in, float* out, const int64_t* shape, int ndim, int axis,
+                     const float* taps, int64_t len) {
+    int64_t inner = 1, outer = 1;
+    for (int j = axis + 1; j < ndim; ++j) inner *= shape[j];
+    for (int j = 0; j < axis; ++j) outer *= shape[j];
+    const int64_t n = shape[axis], mid = len / 2;
+    for (int64_t o = 0; o < outer; ++o)
+        for (int64_t jn = 0; jn < inner; ++jn) {
+            const int64_t base = o * n * inner + jn;
+            for (int64_t k = 0; k < n; ++k) {
+                float sum = -0.0f;
+                for (int64_t i = 0; i < len; ++i) {
+                    int64_t p = k + i >= mid ? k + i - mid : 0;
+                    if (p > n - 1) p = n - 1;
+                    const float prod = in[base + p * inner] * taps[i];
+                    sum = sum + prod;
+                }
+                out[base + k * inner] = sum;
+            }
+        }
+}
+
+int oracle_gaussian_apply_ndarray(float* v, const int64_t* shape, int ndim, const float* sigma,
+                                  const int64_t* half) {
+    if (ndim < 1 || ndim > OR_MAXDIM) return -1;
+    const int64_t nel = numel(shape, ndim);
+    if (nel == 0) return 0;
+    float* tmp = (float*)malloc(sizeof(float) * nel);
+    float* a = v; /* current input */
+    float* b = tmp;
+    for (int d = 0; d < ndim; ++d) {
+        float* taps = (float*)malloc(sizeof(float) * (2 * half[d] + 1));
+        const int64_t len = oracle_gaussian_kernel(sigma[d], half[d], taps);
+        gauss_1d(a, b, shape, ndim, d, taps, len);
+        free(taps);
+        float* t = a; a = b; b = t; /* the pass output becomes the next input */
+    }
+    if (a != v) memcpy(v, a, sizeof(float) * nel);
+    free(tmp);
+    return 0;
+}
+
+int oracle_gaussian_apply(const float* in, float* out, const int64_t* shape, int ndim,
+                          const int64_t* chunk_shape, const float* sigma, const int64_t* half) {
+    if (ndim < 1 || ndim > OR_MAXDIM) return -1;
+    int64_t grid[OR_MAXDIM], nchunks = 1;
+    for (int j = 0; j < ndim; ++j) {
+        if (chunk_shape[j] <= 0 || half[j] < 0) return -1;
+        grid[j] = (shape[j] + chunk_shape[j] - 1) / chunk_shape[j];
+        nchunks *= grid[j];
+    }
+    for (int64_t c = 0; c < nchunks; ++c) {
+        int64_t cidx[OR_MAXDIM], o_start[OR_MAXDIM], o_end[OR_MAXDIM];
+        int64_t i_start[OR_MAXDIM], i_shape[OR_MAXDIM], d_start[OR_MAXDIM], o_shape[OR_MAXDIM];
+        unravel(c, grid, ndim, cidx);
+        for (int j = 0; j < ndim; ++j) {
+            o_start[j] = cidx[j] * chunk_shape[j];
+            const int64_t e = o_start[j] + chunk_shape[j];
+            o_end[j] = e < shape[j] ? e : shape[j];
+            /* ArraySubsetOverlap::new(shape, subset, kernel_half_size) (gaussian.rs:86-87) */
+            i_start[j] = o_start[j] > half[j] ? o_start[j] - half[j] : 0;
+            const int64_t ie = o_end[j] + half[j];
+            i_shape[j] = (ie < shape[j] ? ie : shape[j]) - i_start[j];
+            d_start[j] = o_start[j] - i_start[j];
+            o_shape[j] = o_end[j] - o_start[j];
+        }
+        const int64_t nin = numel(i_shape, ndim), nout = numel(o_shape, ndim);
+        float* block = (float*)malloc(sizeof(float) * (nin > 0 ? nin : 1));
+        int64_t idx[OR_MAXDIM];
+        for (int64_t lin = 0; lin < nin; ++lin) {
+            unravel(lin, i_shape, ndim, idx);
+            int64_t off = 0;
+            for (int j = 0; j < ndim; ++j) off = off * shape[j] + (i_start[j] + idx[j]);
+            block[lin] = in[off];
+        }
+        oracle_gaussian_apply_ndarray(block, i_shape, ndim, sigma, half);
+        for (int64_t lin = 0; lin < nout; ++lin) {
+            unravel(lin, o_shape, ndim, idx);
+            int64_t src = 0, dst = 0;
+            for (int j = 0; j < ndim; ++j) {
+                src = src * i_shape[j] + (d_start[j] + idx[j]);
+                dst = dst * shape[j] + (o_start[j] + idx[j]);
+            }
+            out[dst] = block[src];
+        }
+        free(block);
+    }
+    return 0;
+}

@@ -102,6 +102,20 @@ double oracle_guided_filter_time_chunks(const int64_t* global_shape, const int64
 void oracle_synth_u16(uint16_t* out, const int64_t* shape, int ndim,
                       const int64_t* global_shape, int64_t z0, uint64_t seed);
 
+
+/* gaussian.rs:252-267 create_sampled_gaussian_kernel: sigma == 0 -> [1]; else
+ * scale * exp(-(n*n as f32) / (2 t)) for n = half..0..half, t = sigma^2,
+ * scale = 1 / sqrt(2 pi t). Writes 2*half+1 taps (1 when sigma == 0); returns the tap count. */
+int64_t oracle_gaussian_kernel(float sigma, int64_t half, float* taps);
+/* gaussian.rs:110-119 + kernel.rs:17-73: for each axis in order, an f32 sequential sum of
+ * input[min(sat_sub(k + i, mid), n - 1)] * tap[i] (replicate edges), in place. */
+int oracle_gaussian_apply_ndarray(float* v, const int64_t* shape, int ndim, const float* sigma,
+                                  const int64_t* half);
+/* gaussian.rs:73-108, :170-249: every chunk of the grid with a kernel_half_size halo
+ * (ArraySubsetOverlap), apply_ndarray, extract. */
+int oracle_gaussian_apply(const float* in, float* out, const int64_t* shape, int ndim,
+                          const int64_t* chunk_shape, const float* sigma, const int64_t* half);
+
 #ifdef __cplusplus
 }
 #endif

@@ -30,8 +30,23 @@ def test_downsample_subcommand_grammar():
 def test_off_path_filter_is_rejected(tmp_path):
     S.create_array(tmp_path / "in", "uint8", (4,), (4,))
     with pytest.raises(_abi.FilterError, match="outside the accelerated path"):
-        ZF.run([{"filter": "gaussian", "input": str(tmp_path / "in"), "output": "x"}],
+        ZF.run([{"filter": "gradient_magnitude", "input": str(tmp_path / "in"), "output": "x"}],
                log=lambda *a: None)
+
+
+def test_gaussian_subcommand_grammar():
+    a = ZF.build_parser().parse_args(["gaussian", "i", "o", "1.0,1.5,2", "3,4,6",
+                                      "--data-type", "float32"])
+    st = ZF._steps_from_cli(a)[0]
+    assert st["filter"] == "gaussian" and st["sigma"] == [1.0, 1.5, 2.0]
+    assert st["kernel_half_size"] == [3, 4, 6] and st["data_type"] == "float32"
+
+
+def test_gaussian_needs_one_sigma_per_axis(tmp_path):
+    S.create_array(tmp_path / "in", "uint8", (4, 4), (4, 4))
+    with pytest.raises(_abi.InvalidParameters, match="one entry per axis"):
+        ZF.run([{"filter": "gaussian", "input": str(tmp_path / "in"), "output": "x",
+                 "sigma": [1.0], "kernel_half_size": [3]}], log=lambda *a: None)
 
 
 def test_first_filter_needs_input():

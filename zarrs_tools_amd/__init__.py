@@ -15,6 +15,7 @@ from .filter import (  # noqa: E402
     Context,
     DeviceArray,
     Downsample,
+    Gaussian,
     GuidedFilter,
     default_context,
     dtype_of,
@@ -28,7 +29,7 @@ from .shard import SlabAssignment, slab_assignment  # noqa: E402
 
 __all__ = [
     "ArraySubset", "ArraySubsetOverlap", "Context", "DeviceArray", "Downsample", "DTYPES",
-    "FilterError", "GuidedFilter", "InvalidParameters", "SlabAssignment", "UnsupportedDataType",
+    "FilterError", "Gaussian", "GuidedFilter", "InvalidParameters", "SlabAssignment", "UnsupportedDataType",
     "default_context", "dtype_of", "lib", "pyramid", "pyramid_level_shapes", "slab_assignment",
     "synth_step_noise_f32", "synth_u16", "torch_dtype",
 ]

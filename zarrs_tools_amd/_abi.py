@@ -106,6 +106,7 @@ def lib() -> ctypes.CDLL:
     i64p = ctypes.POINTER(ctypes.c_int64)
     vp = ctypes.c_void_p
     c_int, c_float = ctypes.c_int, ctypes.c_float
+    fp = ctypes.POINTER(ctypes.c_float)
     sig = {
         "zt_abi_version": ([], c_int),
         "zt_last_error": ([], ctypes.c_char_p),
@@ -139,6 +140,14 @@ def lib() -> ctypes.CDLL:
                                     c_int),
         "zt_pyramid_downsample": ([vp, c_int, vp, i64p, c_int, i64p, c_int, c_int,
                                    ctypes.POINTER(vp), ctypes.POINTER(c_int)], c_int),
+        "zt_gaussian_kernel": ([c_float, ctypes.c_int64, fp, i64p], c_int),
+        "zt_gaussian_is_compatible": ([c_int, c_int], c_int),
+        "zt_gaussian_memory_per_chunk": ([c_int, c_int, i64p, c_int, i64p,
+                                          ctypes.POINTER(ctypes.c_uint64)], c_int),
+        "zt_gaussian_apply_ndarray": ([vp, c_int, vp, i64p, c_int, i64p, i64p, c_int, vp, fp,
+                                       i64p], c_int),
+        "zt_gaussian_apply_array": ([vp, c_int, vp, c_int, vp, i64p, c_int, i64p, fp, i64p],
+                                    c_int),
         "zt_synth_step_noise_f32": ([vp, vp, i64p, c_int, i64p, ctypes.c_int64, ctypes.c_uint64],
                                     c_int),
         "zt_synth_u16": ([vp, vp, i64p, c_int, i64p, ctypes.c_int64, ctypes.c_uint64], c_int),
@@ -157,6 +166,12 @@ def lib() -> ctypes.CDLL:
         "zt_store_downsample": ([ctypes.c_char_p, ctypes.c_char_p, i64p, c_int, c_int, c_int,
                                  ctypes.c_int64, ctypes.c_int64, c_int, c_int,
                                  ctypes.POINTER(StoreStats)], c_int),
+        "zt_store_gaussian": ([ctypes.c_char_p, ctypes.c_char_p, c_int, fp, i64p, c_int,
+                               ctypes.c_int64, ctypes.c_int64, c_int, c_int,
+                               ctypes.POINTER(StoreStats)], c_int),
+        "zt_store_downsample_gaussian": ([ctypes.c_char_p, ctypes.c_char_p, i64p, fp, i64p, c_int,
+                                          c_int, ctypes.c_int64, ctypes.c_int64, c_int, c_int,
+                                          ctypes.POINTER(StoreStats)], c_int),
         "zt_store_codec_available": ([ctypes.c_char_p], c_int),
     }
     for name, (args, res) in sig.items():

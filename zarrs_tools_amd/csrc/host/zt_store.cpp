@@ -795,6 +795,126 @@ int zt_store_downsample(const char* in_path, const char* out_path, const int64_t
     }
 }
 
+int zt_store_gaussian(const char* in_path, const char* out_path, int dtype_out, const float* sigma,
+                      const int64_t* kernel_half_size, int device, int64_t row_begin,
+                      int64_t row_end, int nthreads, int flags, zt_store_stats* stats) {
+    try {
+        if (!in_path || !out_path || !sigma || !kernel_half_size)
+            return zt::set_last_error(ZT_ERR_INVALID_PARAMETERS, "null argument");
+        Array in = Array::open(in_path);
+        const int nd = in.ndim();
+        const int dt = dtype_out < 0 ? in.dtype : dtype_out;
+        if (int rc = zt_gaussian_is_compatible(in.dtype, dt)) return rc;
+        for (int d = 0; d < nd; ++d)
+            if (kernel_half_size[d] < 0)
+                return zt::set_last_error(ZT_ERR_INVALID_PARAMETERS, "negative kernel_half_size");
+        Array out = Array::create(out_path, dt, in.shape, in.chunk_shape, in.codecs.to_json(),
+                                  dt == in.dtype ? in.fill_json : convert_fill(in, dt));
+        if (flags & ZT_STORE_ERASE_OUTPUT_METADATA) out.erase_metadata();
+        const int64_t halo = kernel_half_size[0], nz = in.shape[0];
+        RowOp op;
+        op.input_planes = [&](int64_t z0, int64_t z1, int64_t& a, int64_t& b) {
+            a = std::max<int64_t>(0, z0 - halo);  // ArraySubsetOverlap (gaussian.rs:86-87)
+            b = std::min(nz, z1 + halo);
+        };
+        const std::vector<int64_t> shape = in.shape;
+        const std::vector<float> sg(sigma, sigma + nd);
+        const std::vector<int64_t> hs(kernel_half_size, kernel_half_size + nd);
+        const int din = in.dtype;
+        op.apply = [&](zt_ctx* c, const void* slab, int64_t in0, int64_t in1, void* o, int64_t z0,
+                       int64_t z1) -> int {
+            // the slab is a block that carries the halo or reaches the array edge on axis 0 and
+            // spans the other axes: its result on [z0, z1) is the chunked result
+            std::vector<int64_t> bshape(shape), ostart(nd, 0), oshape(shape);
+            bshape[0] = in1 - in0;
+            ostart[0] = z0 - in0;
+            oshape[0] = z1 - z0;
+            return zt_gaussian_apply_ndarray(c, din, slab, bshape.data(), nd, ostart.data(),
+                                             oshape.data(), dt, o, sg.data(), hs.data());
+        };
+        run_pipeline(in, out, device, row_begin, row_end, nthreads, op, stats);
+        if (flags & ZT_STORE_FINISH_OUTPUT) out.store_metadata();
+        return ZT_OK;
+    } catch (const std::exception& e) {
+        return report(e);
+    }
+}
+
+int zt_store_downsample_gaussian(const char* in_path, const char* out_path, const int64_t* stride,
+                                 const float* sigma, const int64_t* kernel_half_size,
+                                 int dtype_out, int device, int64_t row_begin, int64_t row_end,
+                                 int nthreads, int flags, zt_store_stats* stats) {
+    try {
+        if (!in_path || !out_path || !stride || !sigma || !kernel_half_size)
+            return zt::set_last_error(ZT_ERR_INVALID_PARAMETERS, "null argument");
+        Array in = Array::open(in_path);
+        const int nd = in.ndim();
+        const int dt = dtype_out < 0 ? in.dtype : dtype_out;
+        if (int rc = zt_downsample_is_compatible(zt::kF32, dt, 0)) return rc;
+        for (int d = 0; d < nd; ++d)
+            if (kernel_half_size[d] < 0)
+                return zt::set_last_error(ZT_ERR_INVALID_PARAMETERS, "negative kernel_half_size");
+        std::vector<int64_t> st(stride, stride + nd), oshape(nd), win(nd), ochunk(nd);
+        if (int rc = zt_downsample_output_shape(in.shape.data(), nd, st.data(), oshape.data()))
+            return rc;
+        for (int d = 0; d < nd; ++d) {
+            win[d] = std::min(st[d], in.shape[d]);
+            ochunk[d] = std::min(in.chunk_shape[d], oshape[d]);  // zarrs_ome.rs:549-559
+        }
+        zt::json::Value codecs = in.codecs.to_json();
+        if (in.codecs.sharded) {
+            Array probe = in;
+            for (int d = 0; d < nd; ++d)
+                probe.codecs.inner_shape[d] = std::min(in.codecs.inner_shape[d], ochunk[d]);
+            for (int d = 0; d < nd; ++d)
+                if (ochunk[d] % probe.codecs.inner_shape[d]) probe.codecs.inner_shape[d] = ochunk[d];
+            codecs = probe.codecs.to_json();
+        }
+        Array out = Array::create(out_path, dt, oshape, ochunk, codecs,
+                                  dt == in.dtype ? in.fill_json : convert_fill(in, dt));
+        if (flags & ZT_STORE_ERASE_OUTPUT_METADATA) out.erase_metadata();
+        const int64_t w0 = win[0], halo = kernel_half_size[0], nz = in.shape[0];
+        auto ds_planes = [&](int64_t z0, int64_t z1, int64_t& a, int64_t& b) {
+            a = z0 * w0;  // Downsample::input_subset (downsample.rs:64-70)
+            b = std::min(z1 * w0, nz);
+        };
+        RowOp op;
+        op.input_planes = [&](int64_t z0, int64_t z1, int64_t& a, int64_t& b) {
+            ds_planes(z0, z1, a, b);  // plus the Gaussian halo (zarrs_ome.rs:251-255)
+            a = std::max<int64_t>(0, a - halo);
+            b = std::min(nz, b + halo);
+        };
+        const std::vector<int64_t> ishape = in.shape;
+        const std::vector<float> sg(sigma, sigma + nd);
+        const std::vector<int64_t> hs(kernel_half_size, kernel_half_size + nd);
+        int64_t plane = 1;
+        for (int d = 1; d < nd; ++d) plane *= ishape[d];
+        DevBuf gtmp;  // the Gaussian of one row's downsample input (f32)
+        const int din = in.dtype;
+        op.apply = [&](zt_ctx* c, const void* slab, int64_t in0, int64_t in1, void* o, int64_t z0,
+                       int64_t z1) -> int {
+            int64_t a, b;
+            ds_planes(z0, z1, a, b);
+            if (!gtmp.p) gtmp.alloc(sizeof(float) * (size_t)(w0 * out.chunk_shape[0] * plane));
+            std::vector<int64_t> bshape(ishape), gstart(nd, 0), gshape(ishape);
+            bshape[0] = in1 - in0;
+            gstart[0] = a - in0;
+            gshape[0] = b - a;
+            if (int rc = zt_gaussian_apply_ndarray(c, din, slab, bshape.data(), nd, gstart.data(),
+                                                   gshape.data(), zt::kF32, gtmp.p, sg.data(),
+                                                   hs.data()))
+                return rc;
+            return zt_downsample_apply_ndarray(c, zt::kF32, gtmp.p, gshape.data(), nd, st.data(),
+                                               0, dt, o);
+        };
+        run_pipeline(in, out, device, row_begin, row_end, nthreads, op, stats);
+        if (flags & ZT_STORE_FINISH_OUTPUT) out.store_metadata();
+        return ZT_OK;
+    } catch (const std::exception& e) {
+        return report(e);
+    }
+}
+
 int zt_store_codec_available(const char* name) {
     if (!name) return 0;
     std::string n(name);

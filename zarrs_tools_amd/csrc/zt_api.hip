@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -546,6 +547,158 @@ int zt_guided_filter_apply_slab(zt_ctx* ctx, int dtype_in, const void* in, int d
     int depth = chunk_shape && chunk_shape[0] > 0 ? (int)chunk_shape[0] : (int)out_nz;
     return run_fused3(ctx, dtype_in, in, dom, in_z0, in_nz, sz, sy, ost, osh, dtype_out, out, sz,
                       sy, epsilon, radius, depth);
+}
+
+// ---- Gaussian (gaussian.rs) -------------------------------------------------------------------
+
+namespace {
+
+// create_sampled_gaussian_kernel (gaussian.rs:252-267), operation for operation: t = sigma^2,
+// scale = 1 / sqrt(2 * PI * t), tap(n) = scale * exp(-((n*n) as f32) / (2 * t)) with the
+// platform libm expf (as the reference's f32::exp on Linux); taps = tap(half..1), tap(0..half).
+int64_t gaussian_taps(float sigma, int64_t half, float* taps) {
+    if (sigma == 0.0f) {
+        if (taps) taps[0] = 1.0f;
+        return 1;
+    }
+    if (taps) {
+        const float pi = 3.14159265358979323846f;  // std::f32::consts::PI
+        const float t = sigma * sigma;
+        const float scale = 1.0f / sqrtf(2.0f * pi * t);
+        for (int64_t n = 0; n <= half; ++n) {
+            const float e = scale * expf(-((float)(uint64_t)(n * n) / (2.0f * t)));
+            taps[half - n] = e;
+            taps[half + n] = e;
+        }
+    }
+    return 2 * half + 1;
+}
+
+int gaussian_args_ok(const float* sigma, const int64_t* half, int ndim) {
+    if (!sigma || !half) return fail(ZT_ERR_INVALID_PARAMETERS, "null sigma / kernel_half_size");
+    for (int d = 0; d < ndim; ++d) {
+        if (half[d] < 0) return fail(ZT_ERR_INVALID_PARAMETERS, "negative kernel_half_size");
+        if (gaussian_taps(sigma[d], half[d], nullptr) > zt::kGaussMaxTaps)
+            return fail(ZT_ERR_INVALID_PARAMETERS, "kernel_half_size %lld on axis %d exceeds %d",
+                        (long long)half[d], d, (zt::kGaussMaxTaps - 1) / 2);
+    }
+    return ZT_OK;
+}
+
+// Gaussian::apply_ndarray on a C-order block, writing only the output region: one pass per
+// axis (gaussian.hip), each restricted to what the later passes read, through two f32 scratch
+// buffers; the last pass writes f32 outputs in place, other types through a cast.
+int run_gaussian(zt_ctx* ctx, int dtype_in, const void* in, const int64_t* in_shape, int ndim,
+                 const int64_t* out_start, const int64_t* out_shape, int dtype_out, void* out,
+                 const float* sigma, const int64_t* half) {
+    const int64_t nout = numel(out_shape, ndim);
+    if (nout == 0) return ZT_OK;
+    int64_t cur[ZT_MAX_DIMS];
+    std::copy(in_shape, in_shape + ndim, cur);
+    int64_t maxn = 0;
+    for (int d = 0; d < ndim; ++d) {
+        cur[d] = out_shape[d];
+        maxn = std::max(maxn, numel(cur, ndim));
+    }
+    const bool cast_out = dtype_out != zt::kF32;
+    if (int rc = ctx->ensure_scratch(sizeof(float) * 2 * (size_t)maxn)) return rc;
+    float* bufs[2] = {static_cast<float*>(ctx->scratch), static_cast<float*>(ctx->scratch) + maxn};
+    std::copy(in_shape, in_shape + ndim, cur);
+    const void* src = in;
+    int sdt = dtype_in;
+    if (ctx->timed) ZT_HIP(hipEventRecord(ctx->ev0, ctx->cur));
+    for (int d = 0; d < ndim; ++d) {
+        zt::GaussPass p{};
+        p.outer = numel(cur, d);
+        p.n = cur[d];
+        p.on = out_shape[d];
+        p.o0 = out_start[d];
+        p.inner = numel(cur + d + 1, ndim - d - 1);
+        p.len = (int)gaussian_taps(sigma[d], half[d], p.w);
+        p.mid = p.len / 2;
+        float* dst = (d == ndim - 1 && !cast_out) ? static_cast<float*>(out) : bufs[d & 1];
+        hipError_t e = zt::launch_gaussian_pass(src, sdt, dst, p, ctx->cur);
+        if (e != hipSuccess) return hip_fail(e, "gaussian pass launch");
+        src = dst;
+        sdt = zt::kF32;
+        cur[d] = out_shape[d];
+    }
+    if (ctx->timed) ZT_HIP(hipEventRecord(ctx->ev1, ctx->cur));
+    if (cast_out) {
+        hipError_t e = zt::launch_cast_from_f32_3d(static_cast<const float*>(src), dtype_out, out,
+                                                   0, 0, 1, 1, nout, ctx->cur);
+        if (e != hipSuccess) return hip_fail(e, "gaussian output cast");
+    }
+    return ZT_OK;
+}
+
+}  // namespace
+
+int zt_gaussian_kernel(float sigma, int64_t kernel_half_size, float* taps, int64_t* len) {
+    if (!len || kernel_half_size < 0)
+        return fail(ZT_ERR_INVALID_PARAMETERS, "null len or negative kernel_half_size");
+    *len = gaussian_taps(sigma, kernel_half_size, taps);
+    return ZT_OK;
+}
+
+int zt_gaussian_is_compatible(int dtype_in, int dtype_out) {
+    // gaussian.rs:123-147: every listed type is accepted for input and output.
+    return dtypes_ok(dtype_in, dtype_out);
+}
+
+int zt_gaussian_memory_per_chunk(int dtype_in, int dtype_out, const int64_t* chunk_shape,
+                                 int ndim, const int64_t* kernel_half_size, uint64_t* bytes) {
+    if (int rc = dtypes_ok(dtype_in, dtype_out)) return rc;
+    if (int rc = check_shape(chunk_shape, ndim, "chunk_shape")) return rc;
+    if (!bytes || !kernel_half_size) return fail(ZT_ERR_INVALID_PARAMETERS, "null pointer");
+    // gaussian.rs:149-168
+    uint64_t nin = 1;
+    for (int d = 0; d < ndim; ++d) nin *= (uint64_t)(chunk_shape[d] + 2 * kernel_half_size[d]);
+    const uint64_t nout = (uint64_t)numel(chunk_shape, ndim);
+    *bytes = nin * (zt::dtype_size(dtype_in) + 4 * 2) + nout * (4 + zt::dtype_size(dtype_out));
+    return ZT_OK;
+}
+
+int zt_gaussian_apply_ndarray(zt_ctx* ctx, int dtype_in, const void* in, const int64_t* in_shape,
+                              int ndim, const int64_t* out_start, const int64_t* out_shape,
+                              int dtype_out, void* out, const float* sigma,
+                              const int64_t* kernel_half_size) {
+    if (int rc = check_ctx(ctx)) return rc;
+    if (int rc = dtypes_ok(dtype_in, dtype_out)) return rc;
+    if (int rc = check_shape(in_shape, ndim, "in_shape")) return rc;
+    if (int rc = gaussian_args_ok(sigma, kernel_half_size, ndim)) return rc;
+    if (!out_start || !out_shape) return fail(ZT_ERR_INVALID_PARAMETERS, "null output region");
+    for (int d = 0; d < ndim; ++d)
+        if (out_start[d] < 0 || out_shape[d] < 0 || out_start[d] + out_shape[d] > in_shape[d])
+            return fail(ZT_ERR_INVALID_PARAMETERS, "output region outside the block on axis %d",
+                        d);
+    if (numel(out_shape, ndim) == 0) return ZT_OK;
+    if (!in || !out) return fail(ZT_ERR_INVALID_PARAMETERS, "null data pointer");
+    DeviceGuard g(ctx->device);
+    return run_gaussian(ctx, dtype_in, in, in_shape, ndim, out_start, out_shape, dtype_out, out,
+                        sigma, kernel_half_size);
+}
+
+int zt_gaussian_apply_array(zt_ctx* ctx, int dtype_in, const void* in, int dtype_out, void* out,
+                            const int64_t* shape, int ndim, const int64_t* chunk_shape,
+                            const float* sigma, const int64_t* kernel_half_size) {
+    if (int rc = check_ctx(ctx)) return rc;
+    if (int rc = dtypes_ok(dtype_in, dtype_out)) return rc;
+    if (int rc = check_shape(shape, ndim, "shape")) return rc;
+    if (int rc = gaussian_args_ok(sigma, kernel_half_size, ndim)) return rc;
+    if (!chunk_shape) return fail(ZT_ERR_INVALID_PARAMETERS, "null chunk_shape");
+    for (int d = 0; d < ndim; ++d)
+        if (chunk_shape[d] <= 0)
+            return fail(ZT_ERR_INVALID_PARAMETERS, "chunk extent must be positive");
+    if (numel(shape, ndim) == 0) return ZT_OK;
+    if (!in || !out) return fail(ZT_ERR_INVALID_PARAMETERS, "null data pointer");
+    // Every chunk with its kernel_half_size halo (clamped to the array) equals the whole array
+    // with replicate edges at the array bounds: the taps' mid is the halo, so a window clamps
+    // inside a chunk's block only where it clamps at the array.
+    int64_t zero[ZT_MAX_DIMS] = {0};
+    DeviceGuard g(ctx->device);
+    return run_gaussian(ctx, dtype_in, in, shape, ndim, zero, shape, dtype_out, out, sigma,
+                        kernel_half_size);
 }
 
 // ---- downsample ------------------------------------------------------------------------------

@@ -78,6 +78,17 @@ struct DSParams {
 hipError_t launch_downsample(const void* in, int dtype_in, void* out, int dtype_out,
                              const DSParams& p, bool discrete, hipStream_t s);
 
+// Gaussian pass along one axis (gaussian.hip): input region outer x n x inner (C order), output
+// outer x on x inner with output k reading input positions around o0 + k (replicate edges).
+constexpr int kGaussMaxTaps = 255;  // kernel_half_size <= 127 per axis
+struct GaussPass {
+    int64_t outer, n, on, o0, inner;
+    int len, mid;
+    float w[kGaussMaxTaps];
+};
+hipError_t launch_gaussian_pass(const void* in, int dtype_in, float* out, const GaussPass& p,
+                                hipStream_t s);
+
 // Synthetic inputs
 hipError_t launch_synth_step_noise_f32(float* out, int64_t n, int64_t plane, int64_t nx_row,
                                        int64_t nx_global, int64_t z0, uint64_t seed,

@@ -247,6 +247,99 @@ class GuidedFilter:
             None if chunk_grid_count is None else i64_array(chunk_grid_count)))
 
 
+class Gaussian:
+    """gaussian.rs:49-250 — `Gaussian::new(sigma, kernel_half_size, chunk_limit)`: the separable
+    sampled Gaussian, per axis in order, replicate edges (kernel.rs:17-73)."""
+
+    def __init__(self, sigma: Sequence[float], kernel_half_size: Sequence[int],
+                 chunk_limit: Optional[int] = None):
+        self.sigma = tuple(float(s) for s in sigma)
+        self._half = tuple(int(h) for h in kernel_half_size)
+        if len(self.sigma) != len(self._half):
+            raise _abi.InvalidParameters(_abi.ERR_INVALID_PARAMETERS,
+                                         "sigma and kernel_half_size lengths differ")
+        self.chunk_limit = chunk_limit
+
+    def name(self) -> str:
+        return "gaussian"
+
+    def kernel_half_size(self) -> tuple:
+        return self._half
+
+    def kernel(self, axis: int) -> list:
+        """create_sampled_gaussian_kernel (gaussian.rs:252-267) for one axis."""
+        n = ctypes.c_int64()
+        check(lib().zt_gaussian_kernel(self.sigma[axis], self._half[axis], None, ctypes.byref(n)))
+        taps = (ctypes.c_float * n.value)()
+        check(lib().zt_gaussian_kernel(self.sigma[axis], self._half[axis], taps, ctypes.byref(n)))
+        return list(taps)
+
+    def _args(self, nd: int):
+        if len(self.sigma) != nd:
+            raise _abi.InvalidParameters(_abi.ERR_INVALID_PARAMETERS,
+                                         "sigma / kernel_half_size must have one entry per axis")
+        return (ctypes.c_float * nd)(*self.sigma), i64_array(self._half)
+
+    def is_compatible(self, dtype_in: str, dtype_out: str) -> None:
+        for d in (dtype_in, dtype_out):
+            if d not in DTYPES:
+                raise _abi.UnsupportedDataType(_abi.ERR_UNSUPPORTED_DATA_TYPE,
+                                               f"Unsupported data type {d}")
+        check(lib().zt_gaussian_is_compatible(DTYPES[dtype_in], DTYPES[dtype_out]))
+
+    def memory_per_chunk(self, dtype_in: str, dtype_out: str, chunk_shape) -> int:
+        out = ctypes.c_uint64()
+        check(lib().zt_gaussian_memory_per_chunk(DTYPES[dtype_in], DTYPES[dtype_out],
+                                                 i64_array(chunk_shape), len(chunk_shape),
+                                                 i64_array(self._half), ctypes.byref(out)))
+        return int(out.value)
+
+    def apply_ndarray(self, v, out_subset: Optional[ArraySubset] = None,
+                      dtype_out: Optional[str] = None, ctx: Optional[Context] = None):
+        """gaussian.rs:110-119 (+ extract_subset and the `as` casts of apply_chunk) on a
+        device block; returns `out_subset` of the result (whole block by default)."""
+        torch = _torch()
+        v = v.contiguous()
+        ctx = ctx or default_context(v.device.index)
+        dtype_in = dtype_of(v)
+        dtype_out = dtype_out or dtype_in
+        nd = v.dim()
+        if out_subset is None:
+            out_subset = ArraySubset((0,) * nd, tuple(v.shape))
+        sig, half = self._args(nd)
+        out = torch.empty(out_subset.shape, dtype=torch_dtype(dtype_out), device=v.device)
+        check(lib().zt_gaussian_apply_ndarray(
+            ctx.handle, DTYPES[dtype_in], _ptr(v), i64_array(v.shape), nd,
+            i64_array(out_subset.start), i64_array(out_subset.shape), DTYPES[dtype_out],
+            _ptr(out), sig, half))
+        return out
+
+    def apply_chunk(self, input: DeviceArray, output: DeviceArray, chunk_indices,
+                    ctx: Optional[Context] = None) -> None:
+        """gaussian.rs:73-108 on device-resident arrays."""
+        subset_output = output.chunk_subset_bounded(chunk_indices)
+        overlap = ArraySubsetOverlap(input.shape, subset_output, self._half)
+        si = overlap.subset_input()
+        block = input.data[tuple(slice(s, s + n) for s, n in zip(si.start, si.shape))]
+        res = self.apply_ndarray(block, overlap.subset_dst_in_src(), output.dtype, ctx)
+        output.data[tuple(slice(s, s + n) for s, n in
+                          zip(subset_output.start, subset_output.shape))] = res
+
+    def apply(self, input: DeviceArray, output: DeviceArray,
+              ctx: Optional[Context] = None) -> None:
+        """gaussian.rs:170-249 over every output chunk (one pass over the array)."""
+        if tuple(output.shape) != tuple(input.shape):
+            raise _abi.InvalidParameters(_abi.ERR_INVALID_PARAMETERS,
+                                         "input and output shapes differ")
+        ctx = ctx or default_context(input.data.device.index)
+        nd = len(input.shape)
+        sig, half = self._args(nd)
+        check(lib().zt_gaussian_apply_array(
+            ctx.handle, DTYPES[input.dtype], _ptr(input.data.contiguous()), DTYPES[output.dtype],
+            _ptr(output.data), i64_array(input.shape), nd, i64_array(output.chunk_shape), sig,
+            half))
+
+
 class Downsample:
     """downsample.rs:49-287 — `Downsample::new(stride, discrete, chunk_limit)`."""
 

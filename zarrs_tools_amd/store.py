@@ -162,3 +162,36 @@ def downsample(input_path, output_path, stride, discrete: bool = False,
                                     int(bool(discrete)), _dt(data_type), int(device), r0, r1,
                                     int(nthreads), _flags(erase, finish), ctypes.byref(st)))
     return st.as_dict()
+
+
+def _sigma_half(sigma, kernel_half_size):
+    sigma = [float(x) for x in sigma]
+    half = [int(x) for x in kernel_half_size]
+    return (ctypes.c_float * len(sigma))(*sigma), i64_array(half)
+
+
+def gaussian(input_path, output_path, sigma, kernel_half_size, data_type: Optional[str] = None,
+             device: int = 0, rows=None, nthreads: int = 0, erase: bool = True,
+             finish: bool = True) -> dict:
+    """zarrs_filter gaussian INPUT OUTPUT SIGMA KERNEL_HALF_SIZE [--data-type T]."""
+    st = _abi.StoreStats()
+    r0, r1 = (0, -1) if rows is None else (int(rows[0]), int(rows[1]))
+    sg, hs = _sigma_half(sigma, kernel_half_size)
+    check(lib().zt_store_gaussian(_b(input_path), _b(output_path), _dt(data_type), sg, hs,
+                                  int(device), r0, r1, int(nthreads), _flags(erase, finish),
+                                  ctypes.byref(st)))
+    return st.as_dict()
+
+
+def downsample_gaussian(input_path, output_path, stride, sigma, kernel_half_size,
+                        data_type: Optional[str] = None, device: int = 0, rows=None,
+                        nthreads: int = 0, erase: bool = True, finish: bool = True) -> dict:
+    """One zarrs_ome level with --gaussian-sigma (zarrs_ome.rs:236-271)."""
+    st = _abi.StoreStats()
+    r0, r1 = (0, -1) if rows is None else (int(rows[0]), int(rows[1]))
+    sg, hs = _sigma_half(sigma, kernel_half_size)
+    check(lib().zt_store_downsample_gaussian(_b(input_path), _b(output_path), i64_array(stride),
+                                             sg, hs, _dt(data_type), int(device), r0, r1,
+                                             int(nthreads), _flags(erase, finish),
+                                             ctypes.byref(st)))
+    return st.as_dict()

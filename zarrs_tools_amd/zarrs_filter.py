@@ -5,10 +5,12 @@ accelerates:
 
     python -m zarrs_tools_amd.zarrs_filter [--exists erase|exit] [--tmp DIR] [--chunk-limit N]
         [--device D] [RUN_CONFIG.json] [guided-filter IN OUT EPSILON RADIUS [--data-type T]
-                                        | downsample IN OUT STRIDE [--discrete] [--data-type T]]
+                                        | downsample IN OUT STRIDE [--discrete] [--data-type T]
+                                        | gaussian IN OUT SIGMA KERNEL_HALF_SIZE [--data-type T]]
 
-* subcommand arguments as GuidedFilterArguments (guided_filter.rs:25-33) and
-  DownsampleArguments (downsample.rs:20-33, STRIDE comma delimited);
+* subcommand arguments as GuidedFilterArguments (guided_filter.rs:25-33),
+  DownsampleArguments (downsample.rs:20-33, STRIDE comma delimited) and GaussianArguments
+  (gaussian.rs:22-30, SIGMA and KERNEL_HALF_SIZE comma delimited, one entry per axis);
 * a JSON run config is a list of {"filter": "guided_filter" | "downsample", "input", "output",
   ...args, "data_type"}, with "$name" meaning a named temporary array under --tmp and an omitted
   input meaning the previous filter's output (zarrs_filter.rs:106-138, :338-381);
@@ -16,7 +18,7 @@ accelerates:
 * the output metadata is erased before a filter runs and written when it finishes (:297-313).
 
 Filters outside the accelerated path (reencode, crop, rescale, clamp, equal, replace_value,
-gradient_magnitude, gaussian) are rejected with FilterError::Other: they are out of scope
+gradient_magnitude, summed_area_table) are rejected with FilterError::Other: they are out of scope
 (DESIGN.md §1). `--chunk-limit` sets the number of host worker threads that decode and encode
 chunks (the reference's bound on concurrently processed chunks).
 """
@@ -33,11 +35,15 @@ import time
 from . import _abi
 from . import store as S
 
-ON_PATH = ("guided_filter", "downsample")
+ON_PATH = ("guided_filter", "downsample", "gaussian")
 
 
 def _parse_stride(s: str):
     return [int(x) for x in s.split(",") if x.strip()]
+
+
+def _parse_floats(s: str):
+    return [float(x) for x in s.split(",") if x.strip()]
 
 
 def build_parser() -> argparse.ArgumentParser:
@@ -63,6 +69,13 @@ def build_parser() -> argparse.ArgumentParser:
     d.add_argument("--discrete", action="store_true")
     d.add_argument("--data-type", default=None)
     d.add_argument("--chunk-limit", dest="filter_chunk_limit", type=int, default=None)
+    gs = sub.add_parser("gaussian", help="Apply a Gaussian kernel.")
+    gs.add_argument("input")
+    gs.add_argument("output")
+    gs.add_argument("sigma", type=_parse_floats)
+    gs.add_argument("kernel_half_size", type=_parse_stride)
+    gs.add_argument("--data-type", default=None)
+    gs.add_argument("--chunk-limit", dest="filter_chunk_limit", type=int, default=None)
     return ap
 
 
@@ -74,6 +87,10 @@ def _steps_from_cli(a) -> list:
     if a.filter == "downsample":
         return [{"filter": "downsample", "input": a.input, "output": a.output,
                  "stride": a.stride, "discrete": a.discrete, "data_type": a.data_type,
+                 "chunk_limit": a.filter_chunk_limit}]
+    if a.filter == "gaussian":
+        return [{"filter": "gaussian", "input": a.input, "output": a.output, "sigma": a.sigma,
+                 "kernel_half_size": a.kernel_half_size, "data_type": a.data_type,
                  "chunk_limit": a.filter_chunk_limit}]
     return []
 
@@ -130,6 +147,21 @@ def run(steps: list, exists: str = "erase", tmp: str | None = None,
                 st = S.guided_filter(src, dst, float(step["epsilon"]), int(step["radius"]),
                                      data_type=step.get("data_type"), device=device,
                                      nthreads=threads)
+            elif name == "gaussian":
+                sigma, half = step.get("sigma"), step.get("kernel_half_size")
+                if isinstance(sigma, str):
+                    sigma = _parse_floats(sigma)
+                if isinstance(half, str):
+                    half = _parse_stride(half)
+                if (not sigma or not half or len(sigma) != info.ndim
+                        or len(half) != info.ndim):
+                    raise _abi.InvalidParameters(
+                        _abi.ERR_INVALID_PARAMETERS,
+                        "gaussian sigma and kernel_half_size need one entry per axis")
+                log(f"{i}: gaussian sigma={sigma} kernel_half_size={half} "
+                    f"{src} ({info.data_type} {list(info.shape)}) -> {dst}")
+                st = S.gaussian(src, dst, sigma, half, data_type=step.get("data_type"),
+                                device=device, nthreads=threads)
             else:
                 stride = step.get("stride")
                 if isinstance(stride, str):

@@ -2,20 +2,25 @@
 array, every level computed by the HIP downsample kernel over the store.
 
     python -m zarrs_tools_amd.zarrs_ome INPUT OUTPUT [FACTOR,...] [--max-levels N] [--discrete]
-        [--device D] [--chunk-limit N] [--name NAME]
+        [--gaussian-sigma S,...] [--gaussian-kernel-half-size H,...] [--device D]
+        [--chunk-limit N] [--name NAME]
 
 Follows src/bin/zarrs_ome.rs (0.7.2): level 0 is a copy of the input (:341-366, no reencoding);
 level i is the downsample of level i-1 read back from the output (:515-738) with the output chunk
 shape min(input chunk, output shape) (:549-559); the loop stops when every axis has factor 1 or
 extent 1 (:731-737); each level adds a multiscales dataset with scale = the cumulative factor and
-translation (scale - 1) / 2 (:716-726). Mean downsampling, or the mode with --discrete (ties by
-the smallest value: the documented deviation). Gaussian pyramids
-(--gaussian-sigma) are outside the accelerated path and are rejected.
+translation (scale - 1) / 2 (:716-726). Mean downsampling, the mode with --discrete (ties by
+the smallest value: the documented deviation), or with --gaussian-sigma a Gaussian
+of each level's input before the mean (apply_chunk_continuous_gaussian, :236-271; kernel half
+size default ceil(3 sigma), :494-502; ignored with --discrete, :638-646). The multiscales
+"type" is "mode", "average" or "gaussian" (:468-475); axes are named by the array's dimension
+names, else by index (:431-449).
 """
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import shutil
 import sys
@@ -33,7 +38,10 @@ def build_parser() -> argparse.ArgumentParser:
                     type=lambda s: [int(x) for x in s.split(",")])
     ap.add_argument("--max-levels", type=int, default=10)
     ap.add_argument("--discrete", action="store_true")
-    ap.add_argument("--gaussian-sigma", default=None)
+    ap.add_argument("--gaussian-sigma", default=None,
+                    type=lambda s: [float(x) for x in s.split(",")])
+    ap.add_argument("--gaussian-kernel-half-size", default=None,
+                    type=lambda s: [int(x) for x in s.split(",")])
     ap.add_argument("--name", default=None)
     ap.add_argument("--exists", choices=["erase", "exit"], default="erase")
     ap.add_argument("--device", type=int, default=0)
@@ -43,7 +51,7 @@ def build_parser() -> argparse.ArgumentParser:
 
 def run(input_path, output_path, factor=None, max_levels: int = 10, discrete: bool = False,
         name=None, exists: str = "erase", device: int = 0, nthreads: int = 0,
-        log=print) -> dict:
+        gaussian_sigma=None, gaussian_kernel_half_size=None, log=print) -> dict:
     t0 = time.perf_counter()
     info = S.open_array(input_path)
     nd = info.ndim
@@ -51,6 +59,15 @@ def run(input_path, output_path, factor=None, max_levels: int = 10, discrete: bo
     if len(factor) != nd:
         raise _abi.InvalidParameters(_abi.ERR_INVALID_PARAMETERS,
                                      "downsample factor must match the array rank")
+    gauss = None
+    if gaussian_sigma is not None and not discrete:
+        sigma = [float(s) for s in gaussian_sigma]
+        half = ([int(h) for h in gaussian_kernel_half_size] if gaussian_kernel_half_size
+                else [int(math.ceil(s * 3.0)) for s in sigma])
+        if len(sigma) != nd or len(half) != nd:
+            raise _abi.InvalidParameters(_abi.ERR_INVALID_PARAMETERS,
+                                         "gaussian sigma / kernel half size must match the rank")
+        gauss = (sigma, half)
     if os.path.exists(output_path):
         if exists == "exit":
             raise _abi.FilterError(_abi.ERR_OTHER, f"output {output_path} already exists")
@@ -66,7 +83,12 @@ def run(input_path, output_path, factor=None, max_levels: int = 10, discrete: bo
     for i in range(1, max_levels + 1):
         win = [min(f, s) for f, s in zip(factor, shape)]
         src, dst = os.path.join(output_path, str(i - 1)), os.path.join(output_path, str(i))
-        st = S.downsample(src, dst, factor, discrete=discrete, device=device, nthreads=nthreads)
+        if gauss is not None:
+            st = S.downsample_gaussian(src, dst, factor, gauss[0], gauss[1], device=device,
+                                       nthreads=nthreads)
+        else:
+            st = S.downsample(src, dst, factor, discrete=discrete, device=device,
+                              nthreads=nthreads)
         stats.append(st)
         out = S.open_array(dst)
         scale = [s * w for s, w in zip(scale, win)]
@@ -77,15 +99,19 @@ def run(input_path, output_path, factor=None, max_levels: int = 10, discrete: bo
         shape = list(out.shape)
         if all(f == 1 or s == 1 for f, s in zip(factor, shape)):
             break
-    axes = [{"name": n, "type": "space"} for n in ("z", "y", "x")[-nd:]] if nd <= 3 else \
-        [{"name": f"d{k}"} for k in range(nd)]
+    names = info.dimension_names if getattr(info, "dimension_names", None) else None
+    axes = [{"name": (names[k] if names and names[k] is not None else str(k))}
+            for k in range(nd)]
     group = {"zarr_format": 3, "node_type": "group", "attributes": {"ome": {
         "version": "0.5",
         "multiscales": [{"name": name or os.path.basename(os.path.normpath(input_path)),
                          "axes": axes, "datasets": datasets,
-                         "type": "mode" if discrete else "mean",
-                         "metadata": {"description": "zarrs_tools_amd zarrs_ome",
-                                      "kwargs": {"factor": factor, "discrete": discrete}}}]}}}
+                         "type": "mode" if discrete else ("average" if gauss is None
+                                                          else "gaussian"),
+                         "metadata": {"description": "Created with zarrs_tools_amd zarrs_ome",
+                                      "kwargs": {"factor": factor, "discrete": discrete,
+                                                 "gaussian_sigma": None if gauss is None
+                                                 else gauss[0]}}}]}}}
     with open(os.path.join(output_path, "zarr.json"), "w") as f:
         json.dump(group, f, indent=2)
     log(f"Output {output_path} in {time.perf_counter() - t0:.2f}s")
@@ -94,12 +120,9 @@ def run(input_path, output_path, factor=None, max_levels: int = 10, discrete: bo
 
 def main(argv=None) -> int:
     a = build_parser().parse_args(argv)
-    if a.gaussian_sigma is not None and not a.discrete:
-        print("Error: Gaussian pyramids are outside the accelerated path", file=sys.stderr)
-        return 1
     try:
         run(a.input, a.output, a.factor, a.max_levels, a.discrete, a.name, a.exists, a.device,
-            a.chunk_limit)
+            a.chunk_limit, a.gaussian_sigma, a.gaussian_kernel_half_size)
     except _abi.FilterError as e:
         print(f"Error: {e}", file=sys.stderr)
         return 1
