@@ -1,0 +1,106 @@
+#!/usr/bin/env python3
+"""Device-resident rates of the other rows on the path: the zarrs_ome mean
+pyramid (config P per GPU: a 2048^3 uint16 octant, factor 2, 5 levels) and the Gaussian
+(zarrs_filter gaussian 1.0,1.0,1.0 3,3,3 on 1024^3 f32, docs/zarrs_filter.md:107). One JSON line
+per operation with its HBM roofline fraction and a CPU baseline (the oracle's C restatement,
+one thread, on a bounded sample of the same workload).
+
+Algorithmic bytes: pyramid = every level's input read once + output written once (2 B per u16
+element); Gaussian = 4 B read + 4 B written per voxel (the separable passes' intermediates are
+not credited).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+HBM_PEAK_GBS = 8000.0
+
+
+def timed(fn, stream, reps):
+    import torch
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        fn()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def bench_pyramid(n, reps, levels):
+    import numpy as np
+    import torch
+    import zarrs_tools_amd as zt
+    from oracle import oracle as O
+    ctx = zt.default_context(0)
+    x = zt.synth_u16((n, n, n))
+    torch.cuda.synchronize()
+    shapes = zt.pyramid_level_shapes((n, n, n), (2, 2, 2), levels)
+    ms = timed(lambda: zt.pyramid(x, (2, 2, 2), levels, ctx=ctx),
+               torch.cuda.current_stream(), reps)
+    prev, nbytes = (n, n, n), 0
+    for s in shapes:
+        nbytes += 2 * (int(np.prod(prev)) + int(np.prod(s)))
+        prev = s
+    gbs = nbytes / (ms / 1e3) / 1e9
+    # CPU: the oracle's level-1 downsample of a 256^3 sample (single thread)
+    sample = O.synth_u16((256, 256, 256))
+    t0 = time.perf_counter()
+    O.downsample(sample, "uint16", (2, 2, 2), "uint16")
+    cpu_s = time.perf_counter() - t0
+    return {"op": "zarrs_ome mean pyramid (device-resident)", "config":
+            {"level0": [n] * 3, "dtype": "uint16", "factor": [2, 2, 2], "levels": len(shapes)},
+            "ms": round(ms, 4), "input_gvox_per_s": round(n ** 3 / (ms / 1e3) / 1e9, 3),
+            "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
+                         "algorithmic_bytes": nbytes},
+            "cpu_baseline": {"input_gvox_per_s": round(256 ** 3 / cpu_s / 1e9, 4), "cores": 1,
+                             "kind": "port", "sample": "level 1 of a 256^3 uint16 block, "
+                             "oracle downsample (C restatement of downsample.rs:72-97)"}}
+
+
+def bench_gaussian(n, reps):
+    import torch
+    import zarrs_tools_amd as zt
+    from oracle import oracle as O
+    ctx = zt.default_context(0)
+    x = zt.synth_step_noise_f32((n, n, n))
+    y = torch.empty_like(x)
+    g = zt.Gaussian([1.0] * 3, [3] * 3)
+    a_in, a_out = zt.DeviceArray(x, (256,) * 3), zt.DeviceArray(y, (256,) * 3)
+    ms = timed(lambda: g.apply(a_in, a_out, ctx=ctx), torch.cuda.current_stream(), reps)
+    gbs = n ** 3 * 8 / (ms / 1e3) / 1e9
+    sample = O.synth_step_noise_f32((128, 128, 128))
+    t0 = time.perf_counter()
+    O.gaussian_apply_ndarray(sample, [1.0] * 3, [3] * 3)
+    cpu_s = time.perf_counter() - t0
+    return {"op": "gaussian sigma 1,1,1 half 3,3,3 (device-resident)",
+            "config": {"shape": [n] * 3, "dtype": "float32", "chunk": [256] * 3},
+            "ms": round(ms, 4), "gib_per_s": round(n ** 3 * 4 / 2 ** 30 / (ms / 1e3), 3),
+            "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
+                         "algorithmic_bytes": n ** 3 * 8},
+            "cpu_baseline": {"gib_per_s": round(128 ** 3 * 4 / 2 ** 30 / cpu_s, 4), "cores": 1,
+                             "kind": "port", "sample": "128^3 f32 block, oracle Gaussian (C "
+                             "restatement of gaussian.rs:110-119 / kernel.rs:17-73)"}}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--pyramid-size", type=int, default=2048)
+    ap.add_argument("--gaussian-size", type=int, default=1024)
+    ap.add_argument("--levels", type=int, default=5)
+    ap.add_argument("--reps", type=int, default=3)
+    a = ap.parse_args()
+    print(json.dumps(bench_pyramid(a.pyramid_size, a.reps, a.levels)), flush=True)
+    print(json.dumps(bench_gaussian(a.gaussian_size, a.reps)), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -18,47 +18,74 @@
 
 namespace zt {
 
-template <typename TIn, typename IdxT>
+// Threads along the contiguous axis of each pass: for axes with inner > 1 a thread owns one
+// (outer, k) line position and consecutive threads consecutive inner offsets (coalesced tap
+// reads, one stride of `inner` apart); for the last axis (inner == 1) consecutive threads own
+// consecutive k and their tap windows overlap in L1. No integer division per element: the
+// grid's y / z dimensions enumerate the other coordinates.
+template <typename TIn, bool ALONG_K>
 __global__ __launch_bounds__(256) void gauss_pass_kernel(const TIn* __restrict__ in,
                                                          float* __restrict__ out, GaussPass p) {
-    const IdxT inner = (IdxT)p.inner, on = (IdxT)p.on, n = (IdxT)p.n, o0 = (IdxT)p.o0;
-    const IdxT total = (IdxT)p.outer * on * inner;
+    const int64_t inner = p.inner, on = p.on, n = p.n, o0 = p.o0;
     const int len = p.len, mid = p.mid;
-    for (IdxT e = blockIdx.x * (IdxT)blockDim.x + threadIdx.x; e < total;
-         e += (IdxT)gridDim.x * blockDim.x) {
-        const IdxT j = e % inner, t = e / inner;
-        const IdxT k = t % on, o = t / on;
-        const TIn* base = in + (o * n) * inner + j;
-        const IdxT kin = o0 + k;
-        float sum = -0.0f;  // Iterator::sum::<f32> (kernel.rs:46, :66)
-        for (int i = 0; i < len; ++i) {
-            IdxT q = kin + i - mid;  // min(sat_sub(k + i, mid), n - 1)
-            q = q < 0 ? 0 : q;
-            q = q > n - 1 ? n - 1 : q;
-            sum = sum + Elem<TIn>::to_f32(base[q * inner]) * p.w[i];
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    // rows enumerated by (blockIdx.y, blockIdx.z): (outer, k) pairs or outer lines
+    const int64_t rows = ALONG_K ? p.outer : p.outer * on;
+    for (int64_t r = (int64_t)blockIdx.z * gridDim.y + blockIdx.y; r < rows;
+         r += (int64_t)gridDim.y * gridDim.z) {
+        int64_t o, k, j;
+        if constexpr (ALONG_K) {
+            o = r;
+            k = t;
+            j = 0;
+            if (k >= on) return;
+        } else {
+            o = r / on;  // one division per row, not per element
+            k = r - o * on;
+            j = t;
+            if (j >= inner) return;
         }
-        out[e] = sum;
+        const TIn* base = in + (o * n) * inner + j;
+        const int64_t kin = o0 + k;
+        float sum = -0.0f;  // Iterator::sum::<f32> (kernel.rs:46, :66)
+        // taps in groups of 8: the group's loads are all issued before its (in-order) sums
+        for (int i0 = 0; i0 < len; i0 += 8) {
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                int64_t q = kin + i0 + u - mid;  // min(sat_sub(k + i, mid), n - 1)
+                q = q < 0 ? 0 : q;
+                q = q > n - 1 ? n - 1 : q;
+                v[u] = i0 + u < len ? Elem<TIn>::to_f32(base[q * inner]) : 0.0f;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (i0 + u < len) sum = sum + v[u] * p.w[i0 + u];
+        }
+        out[(o * on + k) * inner + j] = sum;
     }
-}
-
-static int gauss_grid(int64_t n) {
-    int64_t b = (n + 255) / 256;
-    return (int)(b < 65536 ? (b > 0 ? b : 1) : 65536);
 }
 
 hipError_t launch_gaussian_pass(const void* in, int dtype_in, float* out, const GaussPass& p,
                                 hipStream_t s) {
-    const int64_t total = p.outer * p.on * p.inner;
-    if (total == 0) return hipSuccess;
-    const bool small = p.outer * p.n * p.inner < (int64_t)INT32_MAX;
+    if (p.outer * p.on * p.inner == 0) return hipSuccess;
+    const bool along_k = p.inner == 1;
+    const int64_t lanes = along_k ? p.on : p.inner;
+    const int64_t rows = along_k ? p.outer : p.outer * p.on;
+    const int64_t gx = (lanes + 255) / 256;
+    if (gx > 0x7FFFFFFF) return hipErrorInvalidValue;
+    const int64_t gy = rows < 65535 ? rows : 65535;
+    const int64_t gzn = (rows + gy - 1) / gy;
+    const int64_t gz = gzn < 65535 ? gzn : 65535;
+    const dim3 grid((unsigned)gx, (unsigned)gy, (unsigned)gz);
     hipError_t err = hipErrorInvalidValue;
     ZT_DISPATCH_DTYPE(dtype_in, T,
-        if (small)
-            hipLaunchKernelGGL((gauss_pass_kernel<T, int32_t>), dim3(gauss_grid(total)),
-                               dim3(256), 0, s, static_cast<const T*>(in), out, p);
+        if (along_k)
+            hipLaunchKernelGGL((gauss_pass_kernel<T, true>), grid, dim3(256), 0, s,
+                               static_cast<const T*>(in), out, p);
         else
-            hipLaunchKernelGGL((gauss_pass_kernel<T, int64_t>), dim3(gauss_grid(total)),
-                               dim3(256), 0, s, static_cast<const T*>(in), out, p);
+            hipLaunchKernelGGL((gauss_pass_kernel<T, false>), grid, dim3(256), 0, s,
+                               static_cast<const T*>(in), out, p);
         err = hipGetLastError())
     return err;
 }
