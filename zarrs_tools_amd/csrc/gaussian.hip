@@ -7,8 +7,8 @@
 // output range on axes <= d and the whole block on axes > d, so the region shrinks pass by pass
 // (GaussPass: outer x n x inner input, outer x on x inner output, output k reads input o0 + k).
 //
-// HBM-bound in principle (4 B read + 4 B write per element per pass, taps re-read from L1/L2);
-// one thread per output element, consecutive threads along the contiguous axis of the region.
+// HBM-bound in principle (4 B read + 4 B write per element per pass): every pass stages its
+// input windows in LDS so each element is fetched about once (column and row kernels below).
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -66,27 +66,114 @@ __global__ __launch_bounds__(256) void gauss_pass_kernel(const TIn* __restrict__
     }
 }
 
+// Column passes (inner > 1): a thread owns one inner offset j and a segment of SEG consecutive
+// outputs along the axis; it loads the segment's input window once (SEG + len - 1 values, in
+// batches of 8 so the loads overlap) into its own LDS column and sums the taps from there, so
+// each input is read about once from memory instead of len times. Only the owning thread
+// touches its column: no barrier.
+constexpr int kGaussSeg = 16, kGaussColMaxWin = 64;
+template <typename TIn>
+__global__ __launch_bounds__(256) void gauss_col_kernel(const TIn* __restrict__ in,
+                                                        float* __restrict__ out, GaussPass p,
+                                                        int64_t nseg) {
+    extern __shared__ float win[];  // [window][256]
+    const int tid = threadIdx.x, len = p.len, mid = p.mid;
+    const int64_t inner = p.inner, on = p.on, n = p.n;
+    const int64_t j = (int64_t)blockIdx.x * 256 + tid;
+    const bool live = j < inner;
+    for (int64_t r = (int64_t)blockIdx.z * gridDim.y + blockIdx.y; r < p.outer * nseg;
+         r += (int64_t)gridDim.y * gridDim.z) {
+        const int64_t o = r / nseg, s = r - o * nseg;  // uniform per block (scalar)
+        const int64_t k0 = s * kGaussSeg;
+        const int kc = (int)(on - k0 < kGaussSeg ? on - k0 : kGaussSeg);
+        const int nw = kc + len - 1;
+        const TIn* base = in + (o * n) * inner + (live ? j : 0);
+        const int64_t q0 = p.o0 + k0 - mid;
+        for (int w0 = 0; w0 < nw; w0 += 8) {
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                int64_t q = q0 + w0 + u;  // min(sat_sub(k + i, mid), n - 1)
+                q = q < 0 ? 0 : (q > n - 1 ? n - 1 : q);
+                v[u] = (w0 + u < nw) ? Elem<TIn>::to_f32(base[q * inner]) : 0.0f;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (w0 + u < nw) win[(w0 + u) * 256 + tid] = v[u];
+        }
+        if (live) {
+            for (int kk = 0; kk < kc; ++kk) {
+                float sum = -0.0f;  // Iterator::sum::<f32> (kernel.rs:46, :66)
+                for (int i = 0; i < len; ++i) sum = sum + win[(kk + i) * 256 + tid] * p.w[i];
+                out[(o * on + k0 + kk) * inner + j] = sum;
+            }
+        }
+    }
+}
+
+// Row passes (inner == 1, the contiguous axis): a block stages 1024 outputs' input window of one
+// line in LDS with coalesced loads, then each thread sums its outputs' taps from LDS.
+constexpr int kGaussRowTile = 1024;
+template <typename TIn>
+__global__ __launch_bounds__(256) void gauss_row_kernel(const TIn* __restrict__ in,
+                                                        float* __restrict__ out, GaussPass p) {
+    extern __shared__ float tile[];  // kGaussRowTile + len - 1
+    const int tid = threadIdx.x, len = p.len, mid = p.mid;
+    const int64_t on = p.on, n = p.n;
+    const int64_t k0 = (int64_t)blockIdx.x * kGaussRowTile;
+    const int kc = (int)(on - k0 < kGaussRowTile ? on - k0 : kGaussRowTile);
+    const int nw = kc + len - 1;
+    for (int64_t o = (int64_t)blockIdx.z * gridDim.y + blockIdx.y; o < p.outer;
+         o += (int64_t)gridDim.y * gridDim.z) {
+        const TIn* line = in + o * n;
+        const int64_t q0 = p.o0 + k0 - mid;
+        __syncthreads();  // the previous line's tile is consumed
+        for (int w = tid; w < nw; w += 256) {
+            int64_t q = q0 + w;
+            q = q < 0 ? 0 : (q > n - 1 ? n - 1 : q);
+            tile[w] = Elem<TIn>::to_f32(line[q]);
+        }
+        __syncthreads();
+        for (int kk = tid; kk < kc; kk += 256) {
+            float sum = -0.0f;
+            for (int i = 0; i < len; ++i) sum = sum + tile[kk + i] * p.w[i];
+            out[o * on + k0 + kk] = sum;
+        }
+    }
+}
+
+static dim3 rows_grid(int64_t gx, int64_t rows) {
+    const int64_t gy = rows < 65535 ? rows : 65535;
+    const int64_t gzn = (rows + gy - 1) / gy;
+    return dim3((unsigned)gx, (unsigned)gy, (unsigned)(gzn < 65535 ? gzn : 65535));
+}
+
 hipError_t launch_gaussian_pass(const void* in, int dtype_in, float* out, const GaussPass& p,
                                 hipStream_t s) {
     if (p.outer * p.on * p.inner == 0) return hipSuccess;
-    const bool along_k = p.inner == 1;
-    const int64_t lanes = along_k ? p.on : p.inner;
-    const int64_t rows = along_k ? p.outer : p.outer * p.on;
-    const int64_t gx = (lanes + 255) / 256;
-    if (gx > 0x7FFFFFFF) return hipErrorInvalidValue;
-    const int64_t gy = rows < 65535 ? rows : 65535;
-    const int64_t gzn = (rows + gy - 1) / gy;
-    const int64_t gz = gzn < 65535 ? gzn : 65535;
-    const dim3 grid((unsigned)gx, (unsigned)gy, (unsigned)gz);
     hipError_t err = hipErrorInvalidValue;
-    ZT_DISPATCH_DTYPE(dtype_in, T,
-        if (along_k)
-            hipLaunchKernelGGL((gauss_pass_kernel<T, true>), grid, dim3(256), 0, s,
+    if (p.inner == 1) {
+        const int64_t gx = (p.on + kGaussRowTile - 1) / kGaussRowTile;
+        const size_t lds = sizeof(float) * (kGaussRowTile + p.len - 1);
+        ZT_DISPATCH_DTYPE(dtype_in, T,
+            hipLaunchKernelGGL(gauss_row_kernel<T>, rows_grid(gx, p.outer), dim3(256), lds, s,
                                static_cast<const T*>(in), out, p);
-        else
-            hipLaunchKernelGGL((gauss_pass_kernel<T, false>), grid, dim3(256), 0, s,
+            err = hipGetLastError())
+    } else if (kGaussSeg + p.len - 1 <= kGaussColMaxWin) {
+        const int64_t nseg = (p.on + kGaussSeg - 1) / kGaussSeg;
+        const size_t lds = sizeof(float) * 256 * (kGaussSeg + p.len - 1);
+        ZT_DISPATCH_DTYPE(dtype_in, T,
+            hipLaunchKernelGGL(gauss_col_kernel<T>, rows_grid((p.inner + 255) / 256,
+                                                              p.outer * nseg),
+                               dim3(256), lds, s, static_cast<const T*>(in), out, p, nseg);
+            err = hipGetLastError())
+    } else {  // long kernels: one output per thread
+        ZT_DISPATCH_DTYPE(dtype_in, T,
+            hipLaunchKernelGGL((gauss_pass_kernel<T, false>),
+                               rows_grid((p.inner + 255) / 256, p.outer * p.on), dim3(256), 0, s,
                                static_cast<const T*>(in), out, p);
-        err = hipGetLastError())
+            err = hipGetLastError())
+    }
     return err;
 }
 
