@@ -142,6 +142,72 @@ __global__ __launch_bounds__(256) void gauss_row_kernel(const TIn* __restrict__ 
     }
 }
 
+// The y and x passes of one (outer) plane in one kernel: a block stages the input tile its
+// 32 x 64 outputs need, with both coordinates clamped at load (clamping composes: the y pass at
+// a clamped column is the y pass of that column), runs the y pass over the tile's columns into
+// LDS and the x pass from there. Per element the products and their order are those of the two
+// separate passes, so the result is identical; the intermediate never goes to memory.
+constexpr int kYXTy = 32, kYXTx = 64;
+template <typename TIn>
+__global__ __launch_bounds__(256) void gauss_yx_kernel(const TIn* __restrict__ in,
+                                                       float* __restrict__ out, int64_t outer,
+                                                       GaussPass py, GaussPass px) {
+    extern __shared__ float sm[];
+    const int tid = threadIdx.x;
+    const int ly = py.len, lx = px.len;
+    const int th = kYXTy + ly - 1, tw = kYXTx + lx - 1;  // staged input tile
+    float* tile = sm;                                     // [th][tw]
+    float* ybuf = sm + th * tw;                           // [kYXTy][tw]
+    const int64_t ny = py.n, nx = px.n, ony = py.on, onx = px.on;
+    const int64_t y0 = (int64_t)blockIdx.y * kYXTy, x0 = (int64_t)blockIdx.x * kYXTx;
+    const int hy = (int)(ony - y0 < kYXTy ? ony - y0 : kYXTy);
+    const int hx = (int)(onx - x0 < kYXTx ? onx - x0 : kYXTx);
+    for (int64_t o = blockIdx.z; o < outer; o += gridDim.z) {
+        const TIn* plane = in + o * ny * nx;
+        __syncthreads();  // the previous plane's tiles are consumed
+        const int64_t qy0 = py.o0 + y0 - py.mid, qx0 = px.o0 + x0 - px.mid;
+        for (int e = tid; e < th * tw; e += 256) {
+            const int r = e / tw, c = e - r * tw;
+            int64_t qy = qy0 + r, qx = qx0 + c;  // min(sat_sub(k + i, mid), n - 1)
+            qy = qy < 0 ? 0 : (qy > ny - 1 ? ny - 1 : qy);
+            qx = qx < 0 ? 0 : (qx > nx - 1 ? nx - 1 : qx);
+            tile[e] = Elem<TIn>::to_f32(plane[qy * nx + qx]);
+        }
+        __syncthreads();
+        for (int e = tid; e < kYXTy * tw; e += 256) {  // y pass
+            const int r = e / tw, c = e - r * tw;
+            float sum = -0.0f;
+            for (int i = 0; i < ly; ++i) sum = sum + tile[(r + i) * tw + c] * py.w[i];
+            ybuf[e] = sum;
+        }
+        __syncthreads();
+        for (int e = tid; e < kYXTy * kYXTx; e += 256) {  // x pass
+            const int r = e / kYXTx, c = e - r * kYXTx;
+            if (r >= hy || c >= hx) continue;
+            float sum = -0.0f;
+            for (int i = 0; i < lx; ++i) sum = sum + ybuf[r * tw + c + i] * px.w[i];
+            out[(o * ony + y0 + r) * onx + x0 + c] = sum;
+        }
+    }
+}
+
+hipError_t launch_gaussian_yx(const void* in, int dtype_in, float* out, int64_t outer,
+                              const GaussPass& py, const GaussPass& px, hipStream_t s) {
+    if (outer * py.on * px.on == 0) return hipSuccess;
+    if (py.len > kGaussYXMaxLen || px.len > kGaussYXMaxLen) return hipErrorInvalidValue;
+    const int th = kYXTy + py.len - 1, tw = kYXTx + px.len - 1;
+    const size_t lds = sizeof(float) * (size_t)(th * tw + kYXTy * tw);
+    const int64_t gx = (px.on + kYXTx - 1) / kYXTx, gy = (py.on + kYXTy - 1) / kYXTy;
+    if (gx > 0x7FFFFFFF || gy > 65535) return hipErrorInvalidValue;
+    const dim3 grid((unsigned)gx, (unsigned)gy, (unsigned)(outer < 65535 ? outer : 65535));
+    hipError_t err = hipErrorInvalidValue;
+    ZT_DISPATCH_DTYPE(dtype_in, T,
+        hipLaunchKernelGGL(gauss_yx_kernel<T>, grid, dim3(256), lds, s, static_cast<const T*>(in),
+                           out, outer, py, px);
+        err = hipGetLastError())
+    return err;
+}
+
 static dim3 rows_grid(int64_t gx, int64_t rows) {
     const int64_t gy = rows < 65535 ? rows : 65535;
     const int64_t gzn = (rows + gy - 1) / gy;

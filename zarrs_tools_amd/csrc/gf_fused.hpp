@@ -281,6 +281,9 @@ __device__ __forceinline__ float div_by_count(float x, float d, float rcp) {
 // ---- buffer (SRD) loads/stores: 32-bit byte offsets, hardware range check (an offset past
 //      num_records reads 0 / drops the store), no 64-bit address math per access. -----------
 using rsrc_t = __amdgpu_buffer_rsrc_t;
+#ifndef GF_OUT_AUX
+#define GF_OUT_AUX 2  // f32 output stores: 2 = nt (see Buf<float>::store)
+#endif
 constexpr int kBadOff = (int)0x80000000;  // >= num_records of any slice: reads 0, writes drop
 
 __device__ __forceinline__ rsrc_t make_rsrc(const void* base, uint32_t bytes) {
@@ -298,7 +301,7 @@ template <> struct Buf<float> {
     // Output stores are streamed with the non-temporal hint (aux 2 = nt) so they do not evict
     // the input slices the march re-reads from L2 a few steps later.
     __device__ static void store(float v, rsrc_t r, int off) {
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, off, 0, 2);
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, off, 0, GF_OUT_AUX);
     }
 };
 template <> struct Buf<uint16_t> {
@@ -346,7 +349,7 @@ template <> struct Quad<float> {
     __device__ static void store(const float (&v)[4], rsrc_t r, int off) {
         const u32x4 q = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
                          __float_as_uint(v[3])};
-        __builtin_amdgcn_raw_buffer_store_b128(q, r, off, 0, 2);
+        __builtin_amdgcn_raw_buffer_store_b128(q, r, off, 0, GF_OUT_AUX);
     }
 };
 template <> struct Quad<uint16_t> {

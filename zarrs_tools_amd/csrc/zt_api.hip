@@ -607,7 +607,15 @@ int run_gaussian(zt_ctx* ctx, int dtype_in, const void* in, const int64_t* in_sh
     const void* src = in;
     int sdt = dtype_in;
     if (ctx->timed) ZT_HIP(hipEventRecord(ctx->ev0, ctx->cur));
-    for (int d = 0; d < ndim; ++d) {
+    // the last two axes in one fused pass when their kernels fit it (and the y extent fits a grid)
+    const bool fuse_yx = ndim >= 2 &&
+                         gaussian_taps(sigma[ndim - 2], half[ndim - 2], nullptr) <=
+                             zt::kGaussYXMaxLen &&
+                         gaussian_taps(sigma[ndim - 1], half[ndim - 1], nullptr) <=
+                             zt::kGaussYXMaxLen &&
+                         (out_shape[ndim - 2] + 31) / 32 <= 65535;
+    const int nsep = fuse_yx ? ndim - 2 : ndim;
+    for (int d = 0; d < nsep; ++d) {
         zt::GaussPass p{};
         p.outer = numel(cur, d);
         p.n = cur[d];
@@ -622,6 +630,24 @@ int run_gaussian(zt_ctx* ctx, int dtype_in, const void* in, const int64_t* in_sh
         src = dst;
         sdt = zt::kF32;
         cur[d] = out_shape[d];
+    }
+    if (fuse_yx) {
+        const int dy = ndim - 2, dx = ndim - 1;
+        zt::GaussPass py{}, px{};
+        py.n = cur[dy];
+        py.on = out_shape[dy];
+        py.o0 = out_start[dy];
+        py.len = (int)gaussian_taps(sigma[dy], half[dy], py.w);
+        py.mid = py.len / 2;
+        px.n = cur[dx];
+        px.on = out_shape[dx];
+        px.o0 = out_start[dx];
+        px.len = (int)gaussian_taps(sigma[dx], half[dx], px.w);
+        px.mid = px.len / 2;
+        float* dst = !cast_out ? static_cast<float*>(out) : bufs[nsep & 1];
+        hipError_t e = zt::launch_gaussian_yx(src, sdt, dst, numel(cur, dy), py, px, ctx->cur);
+        if (e != hipSuccess) return hip_fail(e, "gaussian y/x pass launch");
+        src = dst;
     }
     if (ctx->timed) ZT_HIP(hipEventRecord(ctx->ev1, ctx->cur));
     if (cast_out) {

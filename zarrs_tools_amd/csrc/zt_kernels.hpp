@@ -88,6 +88,11 @@ struct GaussPass {
 };
 hipError_t launch_gaussian_pass(const void* in, int dtype_in, float* out, const GaussPass& p,
                                 hipStream_t s);
+// The last two axes' passes fused (y then x, tiles staged in LDS): input outer x ny x nx, output
+// outer x py.on x px.on; py / px carry the two axes' taps, lengths, output offsets and extents.
+constexpr int kGaussYXMaxLen = 33;
+hipError_t launch_gaussian_yx(const void* in, int dtype_in, float* out, int64_t outer,
+                              const GaussPass& py, const GaussPass& px, hipStream_t s);
 
 // Synthetic inputs
 hipError_t launch_synth_step_noise_f32(float* out, int64_t n, int64_t plane, int64_t nx_row,
