@@ -22,6 +22,7 @@ sys.path.insert(0, ROOT)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--size", type=int, default=1024)
+    ap.add_argument("--nz", type=int, default=0, help="z extent (default: --size)")
     ap.add_argument("--chunk", type=int, default=256)
     ap.add_argument("--radius", type=int, default=2)
     ap.add_argument("--eps", type=float, default=2500.0)
@@ -39,7 +40,7 @@ def main():
     work = os.path.join(a.dir, f"zt_e2e_{os.getpid()}")
     os.makedirs(work, exist_ok=True)
     pin, pout = os.path.join(work, "in.zarr"), os.path.join(work, "out.zarr")
-    shape, chunk = (a.size,) * 3, (a.chunk,) * 3
+    shape, chunk = (a.nz or a.size, a.size, a.size), (a.chunk,) * 3
     comp = None if a.codec == "bytes" else a.codec
     codecs = S.codecs_json(comp, a.level, (a.shard_inner,) * 3 if a.shard_inner else None)
     try:
