@@ -91,15 +91,59 @@ def bench_gaussian(n, reps):
                              "restatement of gaussian.rs:110-119 / kernel.rs:17-73)"}}
 
 
+def bench_guided4d(shape, chunk, radius, reps):
+    """Config T per GPU: a (T, Z, Y, X) f32 time-series share, chunks
+    (4, 256, 256, 256), eps 2500. 4-D arrays take the separable per-axis path."""
+    import numpy as np
+    import torch
+    import zarrs_tools_amd as zt
+    from oracle import oracle as O
+    ctx = zt.default_context(0)
+    x = zt.synth_step_noise_f32(tuple(shape))
+    y = torch.empty_like(x)
+    g = zt.GuidedFilter(2500.0, radius)
+    a_in, a_out = zt.DeviceArray(x, chunk), zt.DeviceArray(y, chunk)
+    ms = timed(lambda: g.apply(a_in, a_out, ctx=ctx), torch.cuda.current_stream(), reps)
+    n = int(np.prod(shape))
+    gbs = n * 8 / (ms / 1e3) / 1e9
+    sshape = (4, 64, 64, 64)
+    sample = O.synth_step_noise_f32(sshape)
+    t0 = time.perf_counter()
+    O.guided_filter_apply(sample, (4, 32, 32, 32), 2500.0, radius, nthreads=1)
+    cpu_s = time.perf_counter() - t0
+    del x, y
+    torch.cuda.empty_cache()
+    return {"op": f"guided_filter r={radius} 4-D time-series (device-resident)",
+            "config": {"shape": list(shape), "dtype": "float32", "chunk": list(chunk),
+                       "eps": 2500.0},
+            "ms": round(ms, 4), "gib_per_s": round(n * 4 / 2 ** 30 / (ms / 1e3), 3),
+            "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
+                         "algorithmic_bytes": n * 8},
+            "cpu_baseline": {"gib_per_s": round(int(np.prod(sshape)) * 4 / 2 ** 30 / cpu_s, 5),
+                             "cores": 1, "kind": "port",
+                             "sample": f"{list(sshape)} f32 block in (4,32,32,32) chunks, oracle "
+                             "guided filter (C restatement of guided_filter.rs)"}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--pyramid-size", type=int, default=2048)
     ap.add_argument("--gaussian-size", type=int, default=1024)
     ap.add_argument("--levels", type=int, default=5)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--t-shape", type=int, nargs=4, default=[4, 1024, 1024, 1024])
+    ap.add_argument("--only", default="pyramid,gaussian,guided4d")
     a = ap.parse_args()
-    print(json.dumps(bench_pyramid(a.pyramid_size, a.reps, a.levels)), flush=True)
-    print(json.dumps(bench_gaussian(a.gaussian_size, a.reps)), flush=True)
+    only = set(a.only.split(","))
+    if "guided4d" in only:
+        print(json.dumps(bench_guided4d(a.t_shape, (4, 256, 256, 256), 2, a.reps)), flush=True)
+        if only == {"guided4d"}:
+            return
+    if "pyramid" in only:
+        print(json.dumps(bench_pyramid(a.pyramid_size, a.reps, a.levels)), flush=True)
+    if "gaussian" in only:
+        print(json.dumps(bench_gaussian(a.gaussian_size, a.reps)), flush=True)
 
 
 if __name__ == "__main__":

@@ -21,6 +21,12 @@
 #ifndef GF_ORDER
 #define GF_ORDER 0
 #endif
+#ifndef GF_K3
+#define GF_K3 4  // P3 outputs per thread (column segment of the f64 y-window)
+#endif
+#ifndef GF_K4
+#define GF_K4 4  // P4 outputs per thread (row segment of the (a, b) x-window)
+#endif
 
 namespace zt {
 
@@ -417,7 +423,7 @@ struct GFConfig {
     static constexpr int PH = p2m4(E1X);  // Hx  (f64)    P12 writes rows, P3 reads columns
     static constexpr int PA = p2m4(E1X);  // Lab (float2) P3 writes, P4 reads rows
     static constexpr int PB = p2m4(TX);   // Hab (float2) P4 writes rows, P5 reads columns
-    static constexpr int K3 = 4, K4 = 4;
+    static constexpr int K3 = GF_K3, K4 = GF_K4;
     static constexpr int K5 = TX * TY / NT;          // outputs per thread (ring width)
     static constexpr int S3 = (E1Y + K3 - 1) / K3;   // segments per column, P3
     static constexpr int S4 = TX / K4;               // segments per row, P4

@@ -74,203 +74,352 @@ hipError_t launch_guided_fused(const GFParams& p, int dtype_in, int dtype_out, i
 }
 
 // ---------------------------------------------------------------------------------------------
-// Separable N-d path (ndim >= 4 or radius > kFusedMaxRadius): the same arithmetic as the fused
-// kernel, one pass per axis through device scratch.
+// Separable N-d path (ndim >= 4 or radius > kFusedMaxRadius): one window-sum pass per axis
+// through device scratch, the reference's arithmetic with the fused kernel's precision rules.
+//   stage 1: box sums of v in f64 (exact for f32 inputs; u = (f32)U / count bit-exact, as
+//            the reference's f64 SAT), f64 scratch between passes;
+//   stage 2: box sums of a and b with an f64 running sum per pass (exact), rounded to f32 once
+//            per pass.
+// Every pass is a running window sum over a segment of outputs per thread (add the entering
+// element, subtract the leaving one: exact in f64), so a voxel is read (seg + 2r) / seg times
+// per pass instead of 2r + 1. The last axis runs one thread per row segment; every other axis
+// runs one thread per (outer, segment, inner) with inner (the contiguous positions) across the
+// lanes, so loads coalesce. Index math is per block / per thread, never per element.
 // ---------------------------------------------------------------------------------------------
+
+constexpr int kSepSeg = 32;   // outputs per thread along the summed axis
+constexpr int kSepNT = 256;   // threads per block
+
+template <typename TS, typename TD>
+__global__ __launch_bounds__(kSepNT) void nd_col_box_kernel(const TS* __restrict__ src,
+                                                            TD* __restrict__ dst, int64_t outer,
+                                                            int len, int64_t inner, int r,
+                                                            int nseg, int64_t ntile) {
+    // block -> (outer o, segment sg, inner tile it); all block-uniform
+    const int64_t b = blockIdx.x;
+    const int64_t it = b % ntile;
+    const int64_t rest = b / ntile;
+    const int sg = (int)(rest % nseg);
+    const int64_t o = rest / nseg;
+    const int64_t i = it * kSepNT + threadIdx.x;
+    if (o >= outer || i >= inner) return;
+    const int c0 = sg * kSepSeg, c1 = min(c0 + kSepSeg, len);
+    const TS* col = src + o * (int64_t)len * inner + i;
+    TD* dcol = dst + o * (int64_t)len * inner + i;
+    double s = 0.0;
+    const int lo = max(c0 - r, 0), hi = min(c0 + r, len - 1);
+    for (int c = lo; c <= hi; ++c) s += (double)col[(int64_t)c * inner];
+    dcol[(int64_t)c0 * inner] = (TD)s;
+    for (int c = c0 + 1; c < c1; ++c) {
+        if (c + r < len) s += (double)col[(int64_t)(c + r) * inner];
+        if (c - r - 1 >= 0) s -= (double)col[(int64_t)(c - r - 1) * inner];
+        dcol[(int64_t)c * inner] = (TD)s;
+    }
+}
+
+template <typename TS, typename TD>
+__global__ __launch_bounds__(kSepNT) void nd_row_box_kernel(const TS* __restrict__ src,
+                                                            TD* __restrict__ dst, int64_t rows,
+                                                            int len, int r, int nseg) {
+    const int64_t t = blockIdx.x * (int64_t)kSepNT + threadIdx.x;
+    if (t >= rows * nseg) return;
+    const int64_t row = t / nseg;
+    const int sg = (int)(t % nseg);
+    const int c0 = sg * kSepSeg, c1 = min(c0 + kSepSeg, len);
+    const TS* x = src + row * len;
+    TD* d = dst + row * len;
+    double s = 0.0;
+    const int lo = max(c0 - r, 0), hi = min(c0 + r, len - 1);
+    for (int c = lo; c <= hi; ++c) s += (double)x[c];
+    d[c0] = (TD)s;
+    for (int c = c0 + 1; c < c1; ++c) {
+        if (c + r < len) s += (double)x[c + r];
+        if (c - r - 1 >= 0) s -= (double)x[c - r - 1];
+        d[c] = (TD)s;
+    }
+}
+
+// Radii <= kSepDirectMaxR: direct (2R+1)-term f64 sums with no loop-carried dependence, so
+// every load of a thread is independent and in flight together.
+constexpr int kSepDirectMaxR = 8;
+constexpr int kSepColK = 16;    // outputs per thread, column kernel
+constexpr int kSepRowTile = 1024;  // outputs per block, row kernel (4 per thread)
+
+// Column axis: a thread owns kSepColK consecutive outputs of one (outer, inner) column and loads
+// their kSepColK + 2R inputs at once (lanes = consecutive inner positions: coalesced).
+template <int R, typename TS, typename TD>
+__global__ __launch_bounds__(kSepNT) void nd_col_box_direct_kernel(
+    const TS* __restrict__ src, TD* __restrict__ dst, int64_t outer, int len, int64_t inner,
+    int nseg, int64_t ntile) {
+    const int64_t b = blockIdx.x;
+    const int64_t it = b % ntile;
+    const int64_t rest = b / ntile;
+    const int sg = (int)(rest % nseg);
+    const int64_t o = rest / nseg;
+    const int64_t i = it * kSepNT + threadIdx.x;
+    if (o >= outer || i >= inner) return;
+    const int c0 = sg * kSepColK;
+    const TS* col = src + o * (int64_t)len * inner + i;
+    TD* dcol = dst + o * (int64_t)len * inner + i;
+    double x[kSepColK + 2 * R];
+#pragma unroll
+    for (int j = 0; j < kSepColK + 2 * R; ++j) {
+        const int c = c0 - R + j;
+        x[j] = (c >= 0 && c < len) ? (double)col[(int64_t)c * inner] : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < kSepColK; ++k) {
+        double s = x[k];
+#pragma unroll
+        for (int j = 1; j <= 2 * R; ++j) s += x[k + j];
+        if (c0 + k < len) dcol[(int64_t)(c0 + k) * inner] = (TD)s;
+    }
+}
+
+// Last axis: a block stages kSepRowTile + 2R elements of one row in LDS (coalesced), then each
+// thread sums the windows of 4 outputs from LDS.
+template <int R, typename TS, typename TD>
+__global__ __launch_bounds__(kSepNT) void nd_row_box_direct_kernel(const TS* __restrict__ src,
+                                                                   TD* __restrict__ dst,
+                                                                   int len, int64_t ntx) {
+    __shared__ double sh[kSepRowTile + 2 * R];
+    const int64_t b = blockIdx.x;
+    const int64_t row = b / ntx;
+    const int c0 = (int)(b % ntx) * kSepRowTile;
+    const TS* x = src + row * len;
+    TD* d = dst + row * len;
+    for (int j = threadIdx.x; j < kSepRowTile + 2 * R; j += kSepNT) {
+        const int c = c0 - R + j;
+        sh[j] = (c >= 0 && c < len) ? (double)x[c] : 0.0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kSepRowTile / kSepNT; ++k) {
+        const int t = threadIdx.x + k * kSepNT;
+        double s = sh[t];
+#pragma unroll
+        for (int j = 1; j <= 2 * R; ++j) s += sh[t + j];
+        if (c0 + t < len) d[c0 + t] = (TD)s;
+    }
+}
+
+template <int R, typename TS, typename TD>
+static hipError_t nd_box_axis_direct(const TS* src, TD* dst, int64_t outer, int len,
+                                     int64_t inner, hipStream_t s) {
+    if (inner == 1) {
+        const int64_t ntx = (len + kSepRowTile - 1) / kSepRowTile;
+        const int64_t nb = outer * ntx;
+        if (nb > 0x7FFFFFFFLL) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((nd_row_box_direct_kernel<R, TS, TD>), dim3((unsigned)nb),
+                           dim3(kSepNT), 0, s, src, dst, len, ntx);
+    } else {
+        const int nseg = (len + kSepColK - 1) / kSepColK;
+        const int64_t ntile = (inner + kSepNT - 1) / kSepNT;
+        const int64_t nb = outer * nseg * ntile;
+        if (nb > 0x7FFFFFFFLL) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((nd_col_box_direct_kernel<R, TS, TD>), dim3((unsigned)nb),
+                           dim3(kSepNT), 0, s, src, dst, outer, len, inner, nseg, ntile);
+    }
+    return hipGetLastError();
+}
+
+template <int R0, typename TS, typename TD>
+static hipError_t nd_box_axis_direct_dispatch(int r, const TS* src, TD* dst, int64_t outer,
+                                              int len, int64_t inner, hipStream_t s) {
+    if constexpr (R0 > kSepDirectMaxR) {
+        return hipErrorInvalidValue;
+    } else {
+        if (r == R0) return nd_box_axis_direct<R0, TS, TD>(src, dst, outer, len, inner, s);
+        return nd_box_axis_direct_dispatch<R0 + 1, TS, TD>(r, src, dst, outer, len, inner, s);
+    }
+}
+
+// Window sums of src along `axis` of the C-contiguous array g.shape -> dst.
+template <typename TS, typename TD>
+static hipError_t nd_box_axis(const TS* src, TD* dst, const NdGeom& g, int axis, int r,
+                              hipStream_t s) {
+    const int len = (int)g.shape[axis];
+    const int nseg = (len + kSepSeg - 1) / kSepSeg;
+    int64_t inner = 1, outer = 1;
+    for (int d = axis + 1; d < g.ndim; ++d) inner *= g.shape[d];
+    for (int d = 0; d < axis; ++d) outer *= g.shape[d];
+    if (r <= kSepDirectMaxR)
+        return nd_box_axis_direct_dispatch<0, TS, TD>(r, src, dst, outer, len, inner, s);
+    if (inner == 1) {
+        const int64_t nthr = outer * nseg;
+        const int64_t nb = (nthr + kSepNT - 1) / kSepNT;
+        if (nb > 0x7FFFFFFFLL) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((nd_row_box_kernel<TS, TD>), dim3((unsigned)nb), dim3(kSepNT), 0, s,
+                           src, dst, outer, len, r, nseg);
+    } else {
+        const int64_t ntile = (inner + kSepNT - 1) / kSepNT;
+        const int64_t nb = outer * nseg * ntile;
+        if (nb > 0x7FFFFFFFLL) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((nd_col_box_kernel<TS, TD>), dim3((unsigned)nb), dim3(kSepNT), 0, s,
+                           src, dst, outer, len, inner, r, nseg, ntile);
+    }
+    return hipGetLastError();
+}
+
+// Row-per-block helpers: a "row" is one index of every axis but the last. The row's coordinates
+// and its window-count factor are block-uniform; threads walk the last axis.
+struct RowCoord {
+    int64_t c[kMaxDims];
+};
+__device__ __forceinline__ void row_coords(int64_t row, const int64_t* shape, int ndim,
+                                           RowCoord& rc) {
+    for (int d = ndim - 2; d >= 0; --d) {
+        rc.c[d] = row % shape[d];
+        row /= shape[d];
+    }
+}
 
 // Gather the (strided, any dtype) block into a contiguous f32 buffer.
 template <typename TIn>
-__global__ void sep_load_kernel(const TIn* __restrict__ in, float* __restrict__ v, NdGeom g) {
-    int64_t n = g.numel;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        int64_t rem = i, off = 0;
-        for (int d = g.ndim - 1; d >= 0; --d) {
-            int64_t c = rem % g.shape[d];
-            rem /= g.shape[d];
-            off += c * g.in_strides[d];
+__global__ __launch_bounds__(kSepNT) void sep_load_kernel(const TIn* __restrict__ in,
+                                                          float* __restrict__ v, NdGeom g) {
+    const int nd = g.ndim;
+    const int64_t len = g.shape[nd - 1], rows = g.numel / len;
+    for (int64_t row = blockIdx.x; row < rows; row += gridDim.x) {
+        RowCoord rc;
+        row_coords(row, g.shape, nd, rc);
+        int64_t off = 0;
+        for (int d = 0; d < nd - 1; ++d) off += rc.c[d] * g.in_strides[d];
+        for (int64_t x = threadIdx.x; x < len; x += kSepNT)
+            v[row * len + x] = Elem<TIn>::to_f32(in[off + x * g.in_strides[nd - 1]]);
+    }
+}
+
+// u = (f32)U / count; s = (v-u)^2; a = s/(s+eps); b = (1-a)u   (guided_filter.rs:126-137,
+// summed_area_table.rs:398-410)
+__global__ __launch_bounds__(kSepNT) void sep_pointwise_kernel(const float* __restrict__ v,
+                                                               const double* __restrict__ U,
+                                                               float* __restrict__ a_out,
+                                                               float* __restrict__ b_out,
+                                                               NdGeom g, int r, float eps) {
+    const int nd = g.ndim;
+    const int64_t len = g.shape[nd - 1], rows = g.numel / len;
+    for (int64_t row = blockIdx.x; row < rows; row += gridDim.x) {
+        RowCoord rc;
+        row_coords(row, g.shape, nd, rc);
+        int64_t cnt_row = 1;
+        for (int d = 0; d < nd - 1; ++d) cnt_row *= clamped_count((int)rc.c[d], (int)g.shape[d], r);
+        for (int64_t x = threadIdx.x; x < len; x += kSepNT) {
+            const int64_t i = row * len + x;
+            const float cnt = (float)(cnt_row * clamped_count((int)x, (int)len, r));
+            const float u = (float)U[i] / cnt;
+            const float d = v[i] - u;
+            const float sq = d * d;
+            const float a = sq / (sq + eps);
+            a_out[i] = a;
+            b_out[i] = (1.0f - a) * u;
         }
-        v[i] = Elem<TIn>::to_f32(in[off]);
-    }
-}
-
-// Window sum of src along `axis` (C-contiguous layout of g.shape), zero-padded outside, in the
-// same binary-tree order as the fused kernel. `nsrc` sources are summed with the same rule.
-template <int W>
-__global__ void sep_box_axis_kernel(const float* __restrict__ src, float* __restrict__ dst,
-                                    NdGeom g, int axis) {
-    int64_t n = g.numel;
-    int64_t stride = 1;
-    for (int d = g.ndim - 1; d > axis; --d) stride *= g.shape[d];
-    int len = (int)g.shape[axis];
-    constexpr int R = (W - 1) / 2;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        int c = (int)((i / stride) % len);
-        float vin[W];
-#pragma unroll
-        for (int t = 0; t < W; ++t) {
-            int cc = c - R + t;
-            vin[t] = (cc >= 0 && cc < len) ? src[i + (int64_t)(cc - c) * stride] : 0.0f;
-        }
-        float o[1];
-        tree_window_sums<R, 1>(vin, o);
-        dst[i] = o[0];
-    }
-}
-
-__device__ __forceinline__ float nd_count(int64_t i, const NdGeom& g, int r) {
-    int64_t rem = i;
-    int64_t cnt = 1;
-    for (int d = g.ndim - 1; d >= 0; --d) {
-        int c = (int)(rem % g.shape[d]);
-        rem /= g.shape[d];
-        cnt *= clamped_count(c, (int)g.shape[d], r);
-    }
-    return (float)cnt;
-}
-
-// u = S/cnt; s = (v-u)^2; a = s/(s+eps); b = (1-a)u  (guided_filter.rs:127-140)
-__global__ void sep_pointwise_kernel(const float* __restrict__ v, const float* __restrict__ S,
-                                     float* __restrict__ a_out, float* __restrict__ b_out,
-                                     NdGeom g, int r, float eps) {
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < g.numel;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        float u = S[i] / nd_count(i, g, r);
-        float d = v[i] - u;
-        float s = d * d;
-        float a = s / (s + eps);
-        a_out[i] = a;
-        b_out[i] = (1.0f - a) * u;
     }
 }
 
 // out = v*(A/cnt) + B/cnt on the output region, cast to TOut (guided_filter.rs:144-163, :101-102)
 template <typename TOut>
-__global__ void sep_final_kernel(const float* __restrict__ v, const float* __restrict__ A,
-                                 const float* __restrict__ B, TOut* __restrict__ out, NdGeom g,
-                                 int r) {
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < g.out_numel;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        int64_t rem = i, src = 0, dst = 0, mul = 1;
-        for (int d = g.ndim - 1; d >= 0; --d) {
-            int64_t c = rem % g.out_shape[d];
-            rem /= g.out_shape[d];
-            src += (c + g.out_start[d]) * mul;
-            mul *= g.shape[d];
-            dst += c * g.out_strides[d];
+__global__ __launch_bounds__(kSepNT) void sep_final_kernel(const float* __restrict__ v,
+                                                           const float* __restrict__ A,
+                                                           const float* __restrict__ B,
+                                                           TOut* __restrict__ out, NdGeom g,
+                                                           int r) {
+    const int nd = g.ndim;
+    const int64_t olen = g.out_shape[nd - 1], orows = g.out_numel / olen;
+    const int64_t len = g.shape[nd - 1];
+    for (int64_t row = blockIdx.x; row < orows; row += gridDim.x) {
+        RowCoord rc;
+        row_coords(row, g.out_shape, nd, rc);
+        int64_t src = 0, dst = 0, cnt_row = 1;
+        for (int d = 0; d < nd - 1; ++d) {
+            const int64_t c = rc.c[d] + g.out_start[d];
+            src = src * g.shape[d] + c;
+            dst += rc.c[d] * g.out_strides[d];
+            cnt_row *= clamped_count((int)c, (int)g.shape[d], r);
         }
-        float cnt = nd_count(src, g, r);
-        float ma = A[src] / cnt;
-        float mb = B[src] / cnt;
-        out[dst] = from_f32<TOut>(__fadd_rn(__fmul_rn(v[src], ma), mb));
-    }
-}
-
-template <int W>
-static void box_all_axes(float* buf, float* tmp, const NdGeom& g, hipStream_t s, int blocks) {
-    // x (last axis) first, then towards axis 0, ping-ponging through tmp; result lands in buf.
-    float* src = buf;
-    float* dst = tmp;
-    for (int axis = g.ndim - 1; axis >= 0; --axis) {
-        hipLaunchKernelGGL(sep_box_axis_kernel<W>, dim3(blocks), dim3(256), 0, s, src, dst, g,
-                           axis);
-        float* t = src; src = dst; dst = t;
-    }
-    if (src != buf)
-        (void)hipMemcpyAsync(buf, src, sizeof(float) * g.numel, hipMemcpyDeviceToDevice, s);
-}
-
-template <int R>
-static hipError_t sep_boxes(float* S, float* tmp, float* A, float* B, const NdGeom& g,
-                            hipStream_t s, int blocks, int which) {
-    constexpr int W = 2 * R + 1;
-    if (which == 0) box_all_axes<W>(S, tmp, g, s, blocks);
-    else {
-        box_all_axes<W>(A, tmp, g, s, blocks);
-        box_all_axes<W>(B, tmp, g, s, blocks);
-    }
-    return hipGetLastError();
-}
-
-// Large radii (> kSepTreeMaxRadius): sequential left-to-right window sum.
-__global__ void sep_box_axis_seq_kernel(const float* __restrict__ src, float* __restrict__ dst,
-                                        NdGeom g, int axis, int R) {
-    int64_t n = g.numel;
-    int64_t stride = 1;
-    for (int d = g.ndim - 1; d > axis; --d) stride *= g.shape[d];
-    int len = (int)g.shape[axis];
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        int c = (int)((i / stride) % len);
-        int lo = c - R < 0 ? 0 : c - R, hi = c + R > len - 1 ? len - 1 : c + R;
-        float acc = 0.0f;
-        for (int cc = lo; cc <= hi; ++cc) acc += src[i + (int64_t)(cc - c) * stride];
-        dst[i] = acc;
-    }
-}
-
-static void box_all_axes_seq(float* buf, float* tmp, const NdGeom& g, hipStream_t s, int blocks,
-                             int R) {
-    float* src = buf;
-    float* dst = tmp;
-    for (int axis = g.ndim - 1; axis >= 0; --axis) {
-        hipLaunchKernelGGL(sep_box_axis_seq_kernel, dim3(blocks), dim3(256), 0, s, src, dst, g,
-                           axis, R);
-        float* t = src; src = dst; dst = t;
-    }
-    if (src != buf)
-        (void)hipMemcpyAsync(buf, src, sizeof(float) * g.numel, hipMemcpyDeviceToDevice, s);
-}
-
-template <int R0 = 0>
-static hipError_t sep_boxes_dispatch(int r, float* S, float* tmp, float* A, float* B,
-                                     const NdGeom& g, hipStream_t s, int blocks, int which) {
-    if constexpr (R0 > kSepTreeMaxRadius) {
-        if (which == 0) box_all_axes_seq(S, tmp, g, s, blocks, r);
-        else {
-            box_all_axes_seq(A, tmp, g, s, blocks, r);
-            box_all_axes_seq(B, tmp, g, s, blocks, r);
+        src = src * len + g.out_start[nd - 1];
+        for (int64_t x = threadIdx.x; x < olen; x += kSepNT) {
+            const int64_t i = src + x;
+            const int gx = (int)(x + g.out_start[nd - 1]);
+            const float cnt = (float)(cnt_row * clamped_count(gx, (int)len, r));
+            const float ma = A[i] / cnt;
+            const float mb = B[i] / cnt;
+            out[dst + x * g.out_strides[nd - 1]] = from_f32<TOut>(__fadd_rn(__fmul_rn(v[i], ma), mb));
         }
-        return hipGetLastError();
-    } else {
-        if (r == R0) return sep_boxes<R0>(S, tmp, A, B, g, s, blocks, which);
-        return sep_boxes_dispatch<R0 + 1>(r, S, tmp, A, B, g, s, blocks, which);
     }
+}
+
+// Box sums along every axis, last axis first (the order of the reference's SAT build is
+// immaterial: f64 sums of f32 values are exact). Returns the buffer holding the result.
+template <typename T0, typename T>
+static hipError_t box_all_axes(const T0* src0, T* p0, T* p1, const NdGeom& g, int r,
+                               hipStream_t s, T** result) {
+    hipError_t e = nd_box_axis<T0, T>(src0, p0, g, g.ndim - 1, r, s);
+    T* cur = p0;
+    T* nxt = p1;
+    for (int axis = g.ndim - 2; axis >= 0 && e == hipSuccess; --axis) {
+        e = nd_box_axis<T, T>(cur, nxt, g, axis, r, s);
+        T* t = cur; cur = nxt; nxt = t;
+    }
+    *result = cur;
+    return e;
 }
 
 hipError_t launch_guided_separable(const void* in, int dtype_in, void* out, int dtype_out,
                                    const NdGeom& g, int radius, float eps, float* scratch,
                                    hipStream_t s) {
-    // scratch: 5 * numel floats: v, S(then reused), A, B, tmp
+    // scratch: 5 * numel floats = v (f32) | region X (2n floats) | region Y (2n floats).
+    // Stage 1 ping-pongs f64 sums between X and Y; a, b (and their pass ping-pong) then use the
+    // region not holding U: A, B in it, A', B' in the other.
     const int64_t n = g.numel;
+    if (n <= 0) return hipSuccess;
     float* v = scratch;
-    float* S = scratch + n;
-    float* A = scratch + 2 * n;
-    float* B = scratch + 3 * n;
-    float* tmp = scratch + 4 * n;
-    int blocks = (int)((n + 255) / 256);
-    if (blocks > 256 * 16) blocks = 256 * 16;
-    if (blocks < 1) blocks = 1;
-    hipError_t err = hipErrorInvalidValue;
-    ZT_DISPATCH_DTYPE(dtype_in, TI,
-        hipLaunchKernelGGL(sep_load_kernel<TI>, dim3(blocks), dim3(256), 0, s,
-                           static_cast<const TI*>(in), v, g);
-        err = hipGetLastError())
+    float* X = scratch + n;
+    float* Y = scratch + 3 * n;
+    const int64_t rows = n / g.shape[g.ndim - 1];
+    const unsigned rblocks = (unsigned)std::min<int64_t>(rows, 1 << 20);
+    // contiguous f32 input is used in place; anything else is gathered into v
+    bool contiguous = dtype_in == kF32;
+    {
+        int64_t st = 1;
+        for (int d = g.ndim - 1; d >= 0; --d) {
+            if (g.in_strides[d] != st) contiguous = false;
+            st *= g.shape[d];
+        }
+    }
+    const float* vin = static_cast<const float*>(in);
+    hipError_t err = hipSuccess;
+    if (!contiguous) {
+        err = hipErrorInvalidValue;
+        ZT_DISPATCH_DTYPE(dtype_in, TI,
+            hipLaunchKernelGGL(sep_load_kernel<TI>, dim3(rblocks), dim3(kSepNT), 0, s,
+                               static_cast<const TI*>(in), v, g);
+            err = hipGetLastError())
+        if (err != hipSuccess) return err;
+        vin = v;
+    }
+    double* U = nullptr;
+    err = box_all_axes<float, double>(vin, reinterpret_cast<double*>(X),
+                                      reinterpret_cast<double*>(Y), g, radius, s, &U);
     if (err != hipSuccess) return err;
-    (void)hipMemcpyAsync(S, v, sizeof(float) * n, hipMemcpyDeviceToDevice, s);
-    err = sep_boxes_dispatch(radius, S, tmp, A, B, g, s, blocks, 0);
-    if (err != hipSuccess) return err;
-    hipLaunchKernelGGL(sep_pointwise_kernel, dim3(blocks), dim3(256), 0, s, v, S, A, B, g,
+    float* free_region = (reinterpret_cast<float*>(U) == X) ? Y : X;
+    float* other = (free_region == X) ? Y : X;  // U's region: free once a, b are made
+    float* A = free_region;
+    float* B = free_region + n;
+    hipLaunchKernelGGL(sep_pointwise_kernel, dim3(rblocks), dim3(kSepNT), 0, s, vin, U, A, B, g,
                        radius, eps);
-    err = sep_boxes_dispatch(radius, S, tmp, A, B, g, s, blocks, 1);
+    if ((err = hipGetLastError()) != hipSuccess) return err;
+    float *Ar = nullptr, *Br = nullptr;
+    err = box_all_axes<float, float>(A, other, A, g, radius, s, &Ar);
     if (err != hipSuccess) return err;
-    int oblocks = (int)((g.out_numel + 255) / 256);
-    if (oblocks > 256 * 16) oblocks = 256 * 16;
-    if (oblocks < 1) oblocks = 1;
+    err = box_all_axes<float, float>(B, other + n, B, g, radius, s, &Br);
+    if (err != hipSuccess) return err;
+    const int64_t orows = g.out_numel / std::max<int64_t>(g.out_shape[g.ndim - 1], 1);
+    if (g.out_numel <= 0) return hipSuccess;
+    const unsigned oblocks = (unsigned)std::min<int64_t>(orows, 1 << 20);
     err = hipErrorInvalidValue;
     ZT_DISPATCH_DTYPE(dtype_out, TO,
-        hipLaunchKernelGGL(sep_final_kernel<TO>, dim3(oblocks), dim3(256), 0, s, v, A, B,
+        hipLaunchKernelGGL(sep_final_kernel<TO>, dim3(oblocks), dim3(kSepNT), 0, s, vin, Ar, Br,
                            static_cast<TO*>(out), g, radius);
         err = hipGetLastError())
     return err;

@@ -491,10 +491,35 @@ int zt_guided_filter_apply_array(zt_ctx* ctx, int dtype_in, const void* in, int 
         return run_fused3(ctx, dtype_in, in, dom, 0, dom[0], sz, sy, ost, osh, dtype_out, obase,
                           sz, sy, epsilon, radius, chunk_depth > 0 ? chunk_depth : 1);
     }
-    // Separable path: chunk by chunk, each reading its 2r halo from the resident array.
-    int64_t nchunks = numel(gn, ndim);
     int64_t ov[ZT_MAX_DIMS];
     for (int d = 0; d < ndim; ++d) ov[d] = (int64_t)((radius * 2) & 0xFF);
+    // Separable path, whole box at once when its scratch (5 f32 words per voxel of the box plus
+    // its 2r halo) fits in half the free device memory: chunked == whole with the halo
+    // (SURVEY.md §0.2), and a contiguous f32 array is then read in place.
+    {
+        int64_t is0[ZT_MAX_DIMS], ish[ZT_MAX_DIMS], dst[ZT_MAX_DIMS];
+        int rc = zt_subset_overlap(shape, ndim, ostart, oshape, ov, is0, ish, dst);
+        if (rc) return rc;
+        size_t free_b = 0, total_b = 0;
+        const size_t need = sizeof(float) * 5 * (size_t)numel(ish, ndim);
+        const bool have = ctx->scratch_bytes >= need ||
+                          (hipMemGetInfo(&free_b, &total_b) == hipSuccess &&
+                           need + ctx->scratch_bytes <= free_b / 2);
+        (void)hipGetLastError();
+        if (have) {
+            int64_t ioff = 0, ooff = 0;
+            for (int d = 0; d < ndim; ++d) {
+                ioff += is0[d] * strides[d];
+                ooff += ostart[d] * strides[d];
+            }
+            return run_separable(ctx, dtype_in, static_cast<const char*>(in) + esz_in * ioff,
+                                 ish, strides, ndim, dst, oshape, dtype_out,
+                                 static_cast<char*>(out) + esz_out * ooff, strides, epsilon,
+                                 radius);
+        }
+    }
+    // Otherwise chunk by chunk, each reading its 2r halo from the resident array.
+    int64_t nchunks = numel(gn, ndim);
     for (int64_t c = 0; c < nchunks; ++c) {
         int64_t rem = c, cs[ZT_MAX_DIMS], csh[ZT_MAX_DIMS];
         for (int d = ndim - 1; d >= 0; --d) {
