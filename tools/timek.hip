@@ -31,7 +31,7 @@ int main(int argc, char** argv) {
     GFParams p{};
     p.in = in; p.out = out; p.in_sz = (int64_t)n * n; p.in_sy = n; p.out_sz = (int64_t)n * n;
     p.out_sy = n; p.in_z0 = 0; p.zlo = 0; p.zhi = n; p.nz = p.ny = p.nx = n;
-    p.oz0 = p.oy0 = p.ox0 = 0; p.onz = p.ony = p.onx = n; p.zseg = argc > 3 ? atoi(argv[3]) : 256; p.eps = 2500.0f;
+    p.oz0 = p.oy0 = p.ox0 = 0; p.onz = p.ony = p.onx = n; p.zseg = (argc > 3 && atoi(argv[3]) > 0) ? atoi(argv[3]) : 256; p.eps = 2500.0f;
     hipStream_t s; CK(hipStreamCreate(&s));
     hipEvent_t a, b;
     CK(hipEventCreate(&a)); CK(hipEventCreate(&b));

@@ -177,41 +177,47 @@ __global__ __launch_bounds__(kSepNT) void nd_col_box_direct_kernel(
 }
 
 // Last axis: a block stages kSepRowTile + 2R elements of one row in LDS (coalesced), then each
-// thread sums the windows of 4 outputs from LDS.
-template <int R, typename TS, typename TD>
+// thread sums the windows of 4 outputs from LDS. P interleaved components per element (P = 2:
+// the (a, b) pairs of stage 2), each summed on its own.
+template <int R, int P, typename TS, typename TD>
 __global__ __launch_bounds__(kSepNT) void nd_row_box_direct_kernel(const TS* __restrict__ src,
                                                                    TD* __restrict__ dst,
                                                                    int len, int64_t ntx) {
-    __shared__ double sh[kSepRowTile + 2 * R];
+    __shared__ double sh[(kSepRowTile + 2 * R) * P];
     const int64_t b = blockIdx.x;
     const int64_t row = b / ntx;
     const int c0 = (int)(b % ntx) * kSepRowTile;
-    const TS* x = src + row * len;
-    TD* d = dst + row * len;
-    for (int j = threadIdx.x; j < kSepRowTile + 2 * R; j += kSepNT) {
-        const int c = c0 - R + j;
-        sh[j] = (c >= 0 && c < len) ? (double)x[c] : 0.0;
+    const TS* x = src + row * len * P;
+    TD* d = dst + row * len * P;
+    for (int j = threadIdx.x; j < (kSepRowTile + 2 * R) * P; j += kSepNT) {
+        const int c = c0 - R + j / P;
+        sh[j] = (c >= 0 && c < len) ? (double)x[(int64_t)c * P + j % P] : 0.0;
     }
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < kSepRowTile / kSepNT; ++k) {
-        const int t = threadIdx.x + k * kSepNT;
-        double s = sh[t];
+    for (int k = 0; k < kSepRowTile * P / kSepNT; ++k) {
+        const int e = threadIdx.x + k * kSepNT;  // element-component index in the tile
+        const int t = e / P, comp = e % P;
+        double s = sh[t * P + comp];
 #pragma unroll
-        for (int j = 1; j <= 2 * R; ++j) s += sh[t + j];
-        if (c0 + t < len) d[c0 + t] = (TD)s;
+        for (int j = 1; j <= 2 * R; ++j) s += sh[(t + j) * P + comp];
+        if (c0 + t < len) d[(int64_t)(c0 + t) * P + comp] = (TD)s;
     }
 }
 
 template <int R, typename TS, typename TD>
 static hipError_t nd_box_axis_direct(const TS* src, TD* dst, int64_t outer, int len,
                                      int64_t inner, hipStream_t s) {
-    if (inner == 1) {
+    if (inner <= 2) {  // last axis (inner = the interleaved components)
         const int64_t ntx = (len + kSepRowTile - 1) / kSepRowTile;
         const int64_t nb = outer * ntx;
         if (nb > 0x7FFFFFFFLL) return hipErrorInvalidValue;
-        hipLaunchKernelGGL((nd_row_box_direct_kernel<R, TS, TD>), dim3((unsigned)nb),
-                           dim3(kSepNT), 0, s, src, dst, len, ntx);
+        if (inner == 1)
+            hipLaunchKernelGGL((nd_row_box_direct_kernel<R, 1, TS, TD>), dim3((unsigned)nb),
+                               dim3(kSepNT), 0, s, src, dst, len, ntx);
+        else
+            hipLaunchKernelGGL((nd_row_box_direct_kernel<R, 2, TS, TD>), dim3((unsigned)nb),
+                               dim3(kSepNT), 0, s, src, dst, len, ntx);
     } else {
         const int nseg = (len + kSepColK - 1) / kSepColK;
         const int64_t ntile = (inner + kSepNT - 1) / kSepNT;
@@ -237,15 +243,15 @@ static hipError_t nd_box_axis_direct_dispatch(int r, const TS* src, TD* dst, int
 // Window sums of src along `axis` of the C-contiguous array g.shape -> dst.
 template <typename TS, typename TD>
 static hipError_t nd_box_axis(const TS* src, TD* dst, const NdGeom& g, int axis, int r,
-                              hipStream_t s) {
+                              hipStream_t s, int P = 1) {
     const int len = (int)g.shape[axis];
     const int nseg = (len + kSepSeg - 1) / kSepSeg;
-    int64_t inner = 1, outer = 1;
+    int64_t inner = P, outer = 1;
     for (int d = axis + 1; d < g.ndim; ++d) inner *= g.shape[d];
     for (int d = 0; d < axis; ++d) outer *= g.shape[d];
     if (r <= kSepDirectMaxR)
         return nd_box_axis_direct_dispatch<0, TS, TD>(r, src, dst, outer, len, inner, s);
-    if (inner == 1) {
+    if (inner == 1) {  // (P = 2 pairs take the column kernel with inner = 2 here: slow, rare)
         const int64_t nthr = outer * nseg;
         const int64_t nb = (nthr + kSepNT - 1) / kSepNT;
         if (nb > 0x7FFFFFFFLL) return hipErrorInvalidValue;
@@ -294,8 +300,7 @@ __global__ __launch_bounds__(kSepNT) void sep_load_kernel(const TIn* __restrict_
 // summed_area_table.rs:398-410)
 __global__ __launch_bounds__(kSepNT) void sep_pointwise_kernel(const float* __restrict__ v,
                                                                const double* __restrict__ U,
-                                                               float* __restrict__ a_out,
-                                                               float* __restrict__ b_out,
+                                                               float2* __restrict__ ab_out,
                                                                NdGeom g, int r, float eps) {
     const int nd = g.ndim;
     const int64_t len = g.shape[nd - 1], rows = g.numel / len;
@@ -311,8 +316,7 @@ __global__ __launch_bounds__(kSepNT) void sep_pointwise_kernel(const float* __re
             const float d = v[i] - u;
             const float sq = d * d;
             const float a = sq / (sq + eps);
-            a_out[i] = a;
-            b_out[i] = (1.0f - a) * u;
+            ab_out[i] = make_float2(a, (1.0f - a) * u);
         }
     }
 }
@@ -320,8 +324,7 @@ __global__ __launch_bounds__(kSepNT) void sep_pointwise_kernel(const float* __re
 // out = v*(A/cnt) + B/cnt on the output region, cast to TOut (guided_filter.rs:144-163, :101-102)
 template <typename TOut>
 __global__ __launch_bounds__(kSepNT) void sep_final_kernel(const float* __restrict__ v,
-                                                           const float* __restrict__ A,
-                                                           const float* __restrict__ B,
+                                                           const float2* __restrict__ AB,
                                                            TOut* __restrict__ out, NdGeom g,
                                                            int r) {
     const int nd = g.ndim;
@@ -342,8 +345,9 @@ __global__ __launch_bounds__(kSepNT) void sep_final_kernel(const float* __restri
             const int64_t i = src + x;
             const int gx = (int)(x + g.out_start[nd - 1]);
             const float cnt = (float)(cnt_row * clamped_count(gx, (int)len, r));
-            const float ma = A[i] / cnt;
-            const float mb = B[i] / cnt;
+            const float2 ab = AB[i];
+            const float ma = ab.x / cnt;
+            const float mb = ab.y / cnt;
             out[dst + x * g.out_strides[nd - 1]] = from_f32<TOut>(__fadd_rn(__fmul_rn(v[i], ma), mb));
         }
     }
@@ -353,12 +357,12 @@ __global__ __launch_bounds__(kSepNT) void sep_final_kernel(const float* __restri
 // immaterial: f64 sums of f32 values are exact). Returns the buffer holding the result.
 template <typename T0, typename T>
 static hipError_t box_all_axes(const T0* src0, T* p0, T* p1, const NdGeom& g, int r,
-                               hipStream_t s, T** result) {
-    hipError_t e = nd_box_axis<T0, T>(src0, p0, g, g.ndim - 1, r, s);
+                               hipStream_t s, T** result, int P = 1) {
+    hipError_t e = nd_box_axis<T0, T>(src0, p0, g, g.ndim - 1, r, s, P);
     T* cur = p0;
     T* nxt = p1;
     for (int axis = g.ndim - 2; axis >= 0 && e == hipSuccess; --axis) {
-        e = nd_box_axis<T, T>(cur, nxt, g, axis, r, s);
+        e = nd_box_axis<T, T>(cur, nxt, g, axis, r, s, P);
         T* t = cur; cur = nxt; nxt = t;
     }
     *result = cur;
@@ -404,23 +408,21 @@ hipError_t launch_guided_separable(const void* in, int dtype_in, void* out, int 
     if (err != hipSuccess) return err;
     float* free_region = (reinterpret_cast<float*>(U) == X) ? Y : X;
     float* other = (free_region == X) ? Y : X;  // U's region: free once a, b are made
-    float* A = free_region;
-    float* B = free_region + n;
-    hipLaunchKernelGGL(sep_pointwise_kernel, dim3(rblocks), dim3(kSepNT), 0, s, vin, U, A, B, g,
-                       radius, eps);
+    float* AB = free_region;                    // (a, b) interleaved: 2n floats
+    hipLaunchKernelGGL(sep_pointwise_kernel, dim3(rblocks), dim3(kSepNT), 0, s, vin, U,
+                       reinterpret_cast<float2*>(AB), g, radius, eps);
     if ((err = hipGetLastError()) != hipSuccess) return err;
-    float *Ar = nullptr, *Br = nullptr;
-    err = box_all_axes<float, float>(A, other, A, g, radius, s, &Ar);
-    if (err != hipSuccess) return err;
-    err = box_all_axes<float, float>(B, other + n, B, g, radius, s, &Br);
+    float* ABr = nullptr;
+    err = box_all_axes<float, float>(AB, other, AB, g, radius, s, &ABr, 2);
     if (err != hipSuccess) return err;
     const int64_t orows = g.out_numel / std::max<int64_t>(g.out_shape[g.ndim - 1], 1);
     if (g.out_numel <= 0) return hipSuccess;
     const unsigned oblocks = (unsigned)std::min<int64_t>(orows, 1 << 20);
     err = hipErrorInvalidValue;
     ZT_DISPATCH_DTYPE(dtype_out, TO,
-        hipLaunchKernelGGL(sep_final_kernel<TO>, dim3(oblocks), dim3(kSepNT), 0, s, vin, Ar, Br,
-                           static_cast<TO*>(out), g, radius);
+        hipLaunchKernelGGL(sep_final_kernel<TO>, dim3(oblocks), dim3(kSepNT), 0, s, vin,
+                           reinterpret_cast<const float2*>(ABr), static_cast<TO*>(out), g,
+                           radius);
         err = hipGetLastError())
     return err;
 }
