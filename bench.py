@@ -38,6 +38,8 @@ def parse():
     ap.add_argument("--size", type=int, default=N, help="per-rank cube edge (default 2048)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-chunks", type=int, default=0, help="chunks in the CPU sample")
+    ap.add_argument("--radius", type=int, default=RADIUS,
+                    help="guided-filter radius (default 4 = the metric; 2 = config G2 at --size 1024)")
     return ap.parse_args()
 
 
@@ -58,7 +60,7 @@ def cpu_baseline(size: int, nchunks: int = 0):
                                             threads)
     gibs = vox * 4 / 2 ** 30 / secs
     return {"value": round(gibs, 5), "unit": "GiB/s", "cores": threads, "kind": "port",
-            "sample": f"{nchunks} chunks of 256^3 (r=4 halo) of the same 2048^3 synthetic "
+            "sample": f"{nchunks} chunks of 256^3 (r={RADIUS} halo) of the same {size}^3 synthetic "
                       f"volume, {secs:.2f} s wall on {threads} threads; C restatement of "
                       f"guided_filter.rs (oracle/zt_oracle.c, faithful incl. dead SAT)"}
 
@@ -77,7 +79,9 @@ def load_traffic(size: int):
 
 
 def main():
+    global RADIUS
     args = parse()
+    RADIUS = args.radius
     import torch
     import torch.distributed as dist
 
@@ -147,7 +151,8 @@ def main():
     traffic = load_traffic(size)
 
     res = {
-        "metric": "GiB/s filtered (device-resident), guided_filter r=4, 2048^3 f32, 256^3 chunks",
+        "metric": f"GiB/s filtered (device-resident), guided_filter r={RADIUS}, {size}^3 f32, "
+                  f"{CHUNK}^3 chunks",
         "value": round(value, 3),
         "unit": "GiB/s",
         "n_gpus": world,

@@ -191,6 +191,99 @@ __global__ __launch_bounds__(256) void gauss_yx_kernel(const TIn* __restrict__ i
     }
 }
 
+// Same passes for f32 input and one odd tap count L on both axes (the common case): taps in
+// registers, staging without divisions, and register windows — a thread makes 4 outputs of a
+// column (y pass) or of a row (x pass) from 4 + L - 1 LDS reads instead of 4L. Every output is
+// still sum = sum + x[i] * w[i] over i = 0..L-1 from -0.0, so the result is bit-identical.
+constexpr int kYXFastTy = 32;  // output rows per block (measured 1024^3: 16 -> 3.86 ms, 32 -> 3.60, 64 -> 5.15)
+template <int L>
+__global__ __launch_bounds__(256) void gauss_yx_fast_kernel(const float* __restrict__ in,
+                                                            float* __restrict__ out,
+                                                            int64_t outer, GaussPass py,
+                                                            GaussPass px) {
+    constexpr int TY = kYXFastTy;
+    constexpr int TH = TY + L - 1, TW = kYXTx + L - 1;
+    __shared__ float tile[TH * TW];
+    __shared__ float ybuf[TY * TW];
+    const int tid = threadIdx.x;
+    float wy[L], wx[L];
+#pragma unroll
+    for (int i = 0; i < L; ++i) {
+        wy[i] = py.w[i];
+        wx[i] = px.w[i];
+    }
+    const int64_t ny = py.n, nx = px.n, ony = py.on, onx = px.on;
+    const int64_t y0 = (int64_t)blockIdx.y * TY, x0 = (int64_t)blockIdx.x * kYXTx;
+    const int hy = (int)(ony - y0 < TY ? ony - y0 : TY);
+    const int hx = (int)(onx - x0 < kYXTx ? onx - x0 : kYXTx);
+    const int64_t qy0 = py.o0 + y0 - py.mid, qx0 = px.o0 + x0 - px.mid;
+    const int tc = tid % 64, tr = tid / 64;  // staging: 4 rows x 64 columns per sweep
+    int64_t qxa = qx0 + tc, qxb = qx0 + 64 + tc;
+    qxa = qxa < 0 ? 0 : (qxa > nx - 1 ? nx - 1 : qxa);
+    qxb = qxb < 0 ? 0 : (qxb > nx - 1 ? nx - 1 : qxb);
+    for (int64_t o = blockIdx.z; o < outer; o += gridDim.z) {
+        const float* plane = in + o * ny * nx;
+        __syncthreads();  // the previous plane's tiles are consumed
+        for (int r = tr; r < TH; r += 4) {
+            int64_t qy = qy0 + r;
+            qy = qy < 0 ? 0 : (qy > ny - 1 ? ny - 1 : qy);
+            const float* row = plane + qy * nx;
+            tile[r * TW + tc] = row[qxa];
+            if (64 + tc < TW) tile[r * TW + 64 + tc] = row[qxb];
+        }
+        __syncthreads();
+        for (int item = tid; item < TW * (TY / 4); item += 256) {  // y pass, 4 rows / item
+            const int c = item % TW, r0 = (item / TW) * 4;
+            float v[4 + L - 1];
+#pragma unroll
+            for (int j = 0; j < 4 + L - 1; ++j) v[j] = tile[(r0 + j) * TW + c];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                float sum = -0.0f;
+#pragma unroll
+                for (int i = 0; i < L; ++i) sum = sum + v[k + i] * wy[i];
+                ybuf[(r0 + k) * TW + c] = sum;
+            }
+        }
+        __syncthreads();
+        for (int item = tid; item < TY * (kYXTx / 4); item += 256) {  // x pass, 4 columns
+            const int r = item / (kYXTx / 4), c0 = (item % (kYXTx / 4)) * 4;
+            if (r >= hy || c0 >= hx) continue;
+            float v[4 + L - 1];
+#pragma unroll
+            for (int j = 0; j < 4 + L - 1; ++j) v[j] = ybuf[r * TW + c0 + j];
+            float o4[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                float sum = -0.0f;
+#pragma unroll
+                for (int i = 0; i < L; ++i) sum = sum + v[k + i] * wx[i];
+                o4[k] = sum;
+            }
+            float* dst = out + (o * ony + y0 + r) * onx + x0 + c0;
+            if (c0 + 4 <= hx && ((uintptr_t)dst & 15) == 0) {
+                *reinterpret_cast<float4*>(dst) = make_float4(o4[0], o4[1], o4[2], o4[3]);
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (c0 + k < hx) dst[k] = o4[k];
+            }
+        }
+    }
+}
+
+template <int L>
+static bool try_gauss_yx_fast(const void* in, int dtype_in, float* out, int64_t outer,
+                              const GaussPass& py, const GaussPass& px, dim3 grid, hipStream_t s,
+                              hipError_t& err) {
+    if (dtype_in != kF32 || py.len != L || px.len != L) return false;
+    const int64_t gy = (py.on + kYXFastTy - 1) / kYXFastTy;
+    hipLaunchKernelGGL(gauss_yx_fast_kernel<L>, dim3(grid.x, (unsigned)gy, grid.z), dim3(256), 0, s,
+                       static_cast<const float*>(in), out, outer, py, px);
+    err = hipGetLastError();
+    return true;
+}
+
 hipError_t launch_gaussian_yx(const void* in, int dtype_in, float* out, int64_t outer,
                               const GaussPass& py, const GaussPass& px, hipStream_t s) {
     if (outer * py.on * px.on == 0) return hipSuccess;
@@ -201,6 +294,13 @@ hipError_t launch_gaussian_yx(const void* in, int dtype_in, float* out, int64_t 
     if (gx > 0x7FFFFFFF || gy > 65535) return hipErrorInvalidValue;
     const dim3 grid((unsigned)gx, (unsigned)gy, (unsigned)(outer < 65535 ? outer : 65535));
     hipError_t err = hipErrorInvalidValue;
+    if (try_gauss_yx_fast<3>(in, dtype_in, out, outer, py, px, grid, s, err) ||
+        try_gauss_yx_fast<5>(in, dtype_in, out, outer, py, px, grid, s, err) ||
+        try_gauss_yx_fast<7>(in, dtype_in, out, outer, py, px, grid, s, err) ||
+        try_gauss_yx_fast<9>(in, dtype_in, out, outer, py, px, grid, s, err) ||
+        try_gauss_yx_fast<11>(in, dtype_in, out, outer, py, px, grid, s, err) ||
+        try_gauss_yx_fast<13>(in, dtype_in, out, outer, py, px, grid, s, err))
+        return err;
     ZT_DISPATCH_DTYPE(dtype_in, T,
         hipLaunchKernelGGL(gauss_yx_kernel<T>, grid, dim3(256), lds, s, static_cast<const T*>(in),
                            out, outer, py, px);
