@@ -195,3 +195,60 @@ def test_256_cube_r4_vs_oracle():
     exact = float(np.mean(out == ref))
     print(f"256^3 r=4: max rel err {err:.3e}, bit-exact fraction {exact:.4f}")
     assert err <= FLOAT_TOL
+
+
+# ---- separable N-d path: 4-D / 5-D arrays and radii > 8 ---------------------
+
+@pytest.mark.parametrize("r", [1, 2, 3, 8, 9, 12])
+def test_separable_4d_vs_oracle_small_eps(r):
+    """Exact f64 stage-1 sums: u matches the reference's even at eps = 0.5, where a 1-ulp error
+    in u moves the output by ~1e-4 relative."""
+    rng = np.random.default_rng(100 + r)
+    shape = (int(rng.integers(3, 7)), int(rng.integers(5, 14)), int(rng.integers(5, 20)),
+             int(rng.integers(5, 40)))
+    chunk = tuple(int(rng.integers(2, 9)) for _ in range(4))
+    v = (rng.random(shape, dtype=np.float32) * 300).astype(np.float32)
+    ref = O.guided_filter_apply(v, chunk, 0.5, r, nthreads=8)
+    out = gpu_apply(v, "float32", "float32", chunk, 0.5, r)
+    assert rel_err(out, ref) <= FLOAT_TOL, (shape, chunk)
+
+
+def test_separable_4d_whole_box_equals_per_chunk():
+    v = O.synth_step_noise_f32((4, 12, 20, 36))
+    chunk = (2, 8, 8, 16)
+    whole = gpu_apply(v, "float32", "float32", chunk, 2500.0, 2)
+    per_chunk = gpu_apply_chunked(v, "float32", "float32", chunk, 2500.0, 2)
+    ref = O.guided_filter_apply(v, chunk, 2500.0, 2, nthreads=8)
+    assert rel_err(whole, ref) <= FLOAT_TOL
+    assert rel_err(per_chunk, ref) <= FLOAT_TOL
+
+
+def test_separable_5d_and_u16_input():
+    rng = np.random.default_rng(5)
+    v32 = (rng.random((3, 4, 5, 6, 18), dtype=np.float32) * 200).astype(np.float32)
+    v = O.cast_from_f32(v32, "uint16")
+    chunk = (2, 2, 4, 4, 8)
+    ref = O.guided_filter_apply(O.cast_to_f32(v, "uint16"), chunk, 50.0, 1, nthreads=8)
+    out = gpu_apply(v, "uint16", "float32", chunk, 50.0, 1)
+    assert rel_err(out, ref) <= FLOAT_TOL
+
+
+@pytest.mark.parametrize("r", [2, 9])
+def test_separable_4d_chunk_grid_subset(r):
+    """A sub-box of the chunk grid: the whole-box launch reads only the box plus its halo and
+    writes only the box."""
+    import torch
+    v = O.synth_step_noise_f32((4, 16, 16, 48))
+    chunk = (2, 8, 8, 16)
+    ref = O.guided_filter_apply(v, chunk, 2500.0, r, nthreads=8)
+    x = to_dev(v, "float32")
+    y = torch.full(v.shape, -1.0, device="cuda")
+    zt.GuidedFilter(2500.0, r).apply(zt.DeviceArray(x, chunk), zt.DeviceArray(y, chunk),
+                                     chunk_grid_start=(1, 0, 1, 1),
+                                     chunk_grid_count=(1, 2, 1, 2))
+    out = from_dev(y, "float32")
+    box = (slice(2, 4), slice(0, 16), slice(8, 16), slice(16, 48))
+    assert rel_err(out[box], ref[box]) <= FLOAT_TOL
+    mask = np.ones(v.shape, bool)
+    mask[box] = False
+    assert np.all(out[mask] == -1)
