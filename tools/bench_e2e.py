@@ -34,6 +34,9 @@ def main():
     ap.add_argument("--repeat", type=int, default=2)
     ap.add_argument("--check", type=int, default=1)
     ap.add_argument("--keep", action="store_true")
+    ap.add_argument("--t", type=int, default=0,
+                    help="4-D time series (config T): T timepoints of nz x size x size")
+    ap.add_argument("--t-chunk", type=int, default=4, help="chunk extent along t (4-D)")
     a = ap.parse_args()
 
     from zarrs_tools_amd import store as S
@@ -41,8 +44,10 @@ def main():
     os.makedirs(work, exist_ok=True)
     pin, pout = os.path.join(work, "in.zarr"), os.path.join(work, "out.zarr")
     shape, chunk = (a.nz or a.size, a.size, a.size), (a.chunk,) * 3
+    if a.t:
+        shape, chunk = (a.t,) + shape, (a.t_chunk,) + chunk
     comp = None if a.codec == "bytes" else a.codec
-    codecs = S.codecs_json(comp, a.level, (a.shard_inner,) * 3 if a.shard_inner else None)
+    codecs = S.codecs_json(comp, a.level, (a.shard_inner,) * len(shape) if a.shard_inner else None)
     try:
         t0 = time.perf_counter()
         S.create_array(pin, "float32", shape, chunk, codecs)
@@ -68,7 +73,21 @@ def main():
             "walls": [round(s["wall_s"], 3) for s in stats],
             "make_input_s": round(t_make, 2),
         }
-        if a.check:
+        if a.check and a.t:
+            # 4-D: a corner sub-box of the first t-chunk row; its block plus the 2r halo makes
+            # the same windows as the whole array (chunked == whole with the halo)
+            import numpy as np
+            from oracle import oracle as O
+            h = 2 * a.radius
+            sub = (a.t_chunk, 16, 16, 64)
+            bshape = tuple(min(s_ + h, n) for s_, n in zip(sub, shape))
+            block = S.read_array(pin, (0,) * 4, bshape)
+            got = S.read_array(pout, (0,) * 4, sub)
+            ref = O.guided_filter_apply_ndarray(block, a.eps, a.radius)[tuple(slice(0, s_) for s_ in sub)]
+            err = float(np.max(np.abs(got.astype(np.float64) - ref) /
+                               np.maximum(1.0, np.abs(ref))))
+            res["check"] = {"sub_box": sub, "max_rel_err": err, "ok": err <= 1e-5}
+        elif a.check:
             import numpy as np
             from oracle import oracle as O
             c = a.chunk
