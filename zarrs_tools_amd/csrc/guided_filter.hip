@@ -142,7 +142,7 @@ __global__ __launch_bounds__(kSepNT) void nd_row_box_kernel(const TS* __restrict
 // Radii <= kSepDirectMaxR: direct (2R+1)-term f64 sums with no loop-carried dependence, so
 // every load of a thread is independent and in flight together.
 constexpr int kSepDirectMaxR = 8;
-constexpr int kSepColK = 16;    // outputs per thread, column kernel
+constexpr int kSepColK = 8;    // outputs per thread, column kernel (4-D T share: 4 -> 164.5 ms, 8 -> 154.8, 16 -> 165.6)
 constexpr int kSepRowTile = 1024;  // outputs per block, row kernel (4 per thread)
 
 // Column axis: a thread owns kSepColK consecutive outputs of one (outer, inner) column and loads
