@@ -176,6 +176,41 @@ __global__ __launch_bounds__(kSepNT) void nd_col_box_direct_kernel(
     }
 }
 
+// f32 pairs (stage 2's interleaved (a, b)): one float2 per lane per load, two f64 sums.
+template <int R>
+__global__ __launch_bounds__(kSepNT) void nd_col_box_pair_kernel(
+    const float2* __restrict__ src, float2* __restrict__ dst, int64_t outer, int len,
+    int64_t inner2, int nseg, int64_t ntile) {
+    const int64_t b = blockIdx.x;
+    const int64_t it = b % ntile;
+    const int64_t rest = b / ntile;
+    const int sg = (int)(rest % nseg);
+    const int64_t o = rest / nseg;
+    const int64_t i = it * kSepNT + threadIdx.x;
+    if (o >= outer || i >= inner2) return;
+    const int c0 = sg * kSepColK;
+    const float2* col = src + o * (int64_t)len * inner2 + i;
+    float2* dcol = dst + o * (int64_t)len * inner2 + i;
+    double xa[kSepColK + 2 * R], xb[kSepColK + 2 * R];
+#pragma unroll
+    for (int j = 0; j < kSepColK + 2 * R; ++j) {
+        const int c = c0 - R + j;
+        const float2 v = (c >= 0 && c < len) ? col[(int64_t)c * inner2] : make_float2(0.f, 0.f);
+        xa[j] = (double)v.x;
+        xb[j] = (double)v.y;
+    }
+#pragma unroll
+    for (int k = 0; k < kSepColK; ++k) {
+        double sa = xa[k], sb = xb[k];
+#pragma unroll
+        for (int j = 1; j <= 2 * R; ++j) {
+            sa += xa[k + j];
+            sb += xb[k + j];
+        }
+        if (c0 + k < len) dcol[(int64_t)(c0 + k) * inner2] = make_float2((float)sa, (float)sb);
+    }
+}
+
 // Last axis: a block stages kSepRowTile + 2R elements of one row in LDS (coalesced), then each
 // thread sums the windows of 4 outputs from LDS. P interleaved components per element (P = 2:
 // the (a, b) pairs of stage 2), each summed on its own.
@@ -220,6 +255,19 @@ static hipError_t nd_box_axis_direct(const TS* src, TD* dst, int64_t outer, int 
                                dim3(kSepNT), 0, s, src, dst, len, ntx);
     } else {
         const int nseg = (len + kSepColK - 1) / kSepColK;
+        if constexpr (std::is_same<TS, float>::value && std::is_same<TD, float>::value) {
+            if (inner % 2 == 0 && ((uintptr_t)src % 8) == 0 && ((uintptr_t)dst % 8) == 0) {
+                const int64_t inner2 = inner / 2;
+                const int64_t ntile2 = (inner2 + kSepNT - 1) / kSepNT;
+                const int64_t nb2 = outer * nseg * ntile2;
+                if (nb2 > 0x7FFFFFFFLL) return hipErrorInvalidValue;
+                hipLaunchKernelGGL((nd_col_box_pair_kernel<R>), dim3((unsigned)nb2), dim3(kSepNT),
+                                   0, s, reinterpret_cast<const float2*>(src),
+                                   reinterpret_cast<float2*>(dst), outer, len, inner2, nseg,
+                                   ntile2);
+                return hipGetLastError();
+            }
+        }
         const int64_t ntile = (inner + kSepNT - 1) / kSepNT;
         const int64_t nb = outer * nseg * ntile;
         if (nb > 0x7FFFFFFFLL) return hipErrorInvalidValue;
