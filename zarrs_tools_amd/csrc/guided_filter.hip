@@ -176,10 +176,11 @@ __global__ __launch_bounds__(kSepNT) void nd_col_box_direct_kernel(
     }
 }
 
-// f32 pairs (stage 2's interleaved (a, b)): one float2 per lane per load, two f64 sums.
-template <int R>
+// Two adjacent inner elements per lane (V2 = float2: stage 2's interleaved (a, b); double2:
+// stage 1's f64 sums): one 8- or 16-byte load per lane per row, two f64 sums.
+template <int R, typename V2>
 __global__ __launch_bounds__(kSepNT) void nd_col_box_pair_kernel(
-    const float2* __restrict__ src, float2* __restrict__ dst, int64_t outer, int len,
+    const V2* __restrict__ src, V2* __restrict__ dst, int64_t outer, int len,
     int64_t inner2, int nseg, int64_t ntile) {
     const int64_t b = blockIdx.x;
     const int64_t it = b % ntile;
@@ -189,13 +190,15 @@ __global__ __launch_bounds__(kSepNT) void nd_col_box_pair_kernel(
     const int64_t i = it * kSepNT + threadIdx.x;
     if (o >= outer || i >= inner2) return;
     const int c0 = sg * kSepColK;
-    const float2* col = src + o * (int64_t)len * inner2 + i;
-    float2* dcol = dst + o * (int64_t)len * inner2 + i;
+    const V2* col = src + o * (int64_t)len * inner2 + i;
+    V2* dcol = dst + o * (int64_t)len * inner2 + i;
     double xa[kSepColK + 2 * R], xb[kSepColK + 2 * R];
 #pragma unroll
     for (int j = 0; j < kSepColK + 2 * R; ++j) {
         const int c = c0 - R + j;
-        const float2 v = (c >= 0 && c < len) ? col[(int64_t)c * inner2] : make_float2(0.f, 0.f);
+        V2 v;
+        if (c >= 0 && c < len) v = col[(int64_t)c * inner2];
+        else v.x = v.y = 0;
         xa[j] = (double)v.x;
         xb[j] = (double)v.y;
     }
@@ -207,7 +210,12 @@ __global__ __launch_bounds__(kSepNT) void nd_col_box_pair_kernel(
             sa += xa[k + j];
             sb += xb[k + j];
         }
-        if (c0 + k < len) dcol[(int64_t)(c0 + k) * inner2] = make_float2((float)sa, (float)sb);
+        if (c0 + k < len) {
+            V2 o2;
+            o2.x = (decltype(o2.x))sa;
+            o2.y = (decltype(o2.y))sb;
+            dcol[(int64_t)(c0 + k) * inner2] = o2;
+        }
     }
 }
 
@@ -255,16 +263,19 @@ static hipError_t nd_box_axis_direct(const TS* src, TD* dst, int64_t outer, int 
                                dim3(kSepNT), 0, s, src, dst, len, ntx);
     } else {
         const int nseg = (len + kSepColK - 1) / kSepColK;
-        if constexpr (std::is_same<TS, float>::value && std::is_same<TD, float>::value) {
-            if (inner % 2 == 0 && ((uintptr_t)src % 8) == 0 && ((uintptr_t)dst % 8) == 0) {
+        if constexpr (std::is_same<TS, TD>::value &&
+                      (std::is_same<TS, float>::value || std::is_same<TS, double>::value)) {
+            using V2 = typename std::conditional<std::is_same<TS, float>::value, float2,
+                                                 double2>::type;
+            if (inner % 2 == 0 && ((uintptr_t)src % sizeof(V2)) == 0 &&
+                ((uintptr_t)dst % sizeof(V2)) == 0) {
                 const int64_t inner2 = inner / 2;
                 const int64_t ntile2 = (inner2 + kSepNT - 1) / kSepNT;
                 const int64_t nb2 = outer * nseg * ntile2;
                 if (nb2 > 0x7FFFFFFFLL) return hipErrorInvalidValue;
-                hipLaunchKernelGGL((nd_col_box_pair_kernel<R>), dim3((unsigned)nb2), dim3(kSepNT),
-                                   0, s, reinterpret_cast<const float2*>(src),
-                                   reinterpret_cast<float2*>(dst), outer, len, inner2, nseg,
-                                   ntile2);
+                hipLaunchKernelGGL((nd_col_box_pair_kernel<R, V2>), dim3((unsigned)nb2),
+                                   dim3(kSepNT), 0, s, reinterpret_cast<const V2*>(src),
+                                   reinterpret_cast<V2*>(dst), outer, len, inner2, nseg, ntile2);
                 return hipGetLastError();
             }
         }
