@@ -1,21 +1,30 @@
 #!/usr/bin/env python3
 """bench.py — device-resident guided_filter throughput (BASELINE.json metric).
 
-Metric: GiB/s filtered (device-resident), guided_filter r=4, 2048^3 f32, 256^3 chunks.
-A step = one pass of the guided filter over every 256^3 chunk of this rank's 2048^3 f32 volume
-(one fused-kernel launch on the HBM-resident array), inputs already resident when timing starts.
+Metric: GiB/s filtered (device-resident), guided_filter r=4, 2048^3 f32, 256^3 chunks
+(BASELINE.json configs[2]; configs[1] is `--size 1024 --radius 2`). A step = one pass of the guided
+filter over every 256^3 output chunk this rank owns (one fused-kernel launch on the HBM-resident
+slab), inputs already resident when timing starts.
 
-Multi-GPU (torchrun, one rank per GPU): weak scaling. The global array is (N*2048, 2048, 2048);
-rank g owns the chunk rows of z in [g*2048, (g+1)*2048) and holds them plus the 2r halo rows the
-reference's per-chunk ArraySubsetOverlap would read, generated on its own device from the global
-synthetic definition. No data-path collective: the process group is used only for the barrier
-and the max-over-ranks of the timed region.
+Multi-GPU (one process per GPU; `--gpus N` launches the N ranks itself through torch.distributed.run
+when it is not already running under a launcher). The chunk work queue is split, as the reference's
+chunk loop would be split (guided_filter.rs:260-316), into contiguous chunk rows along axis 0:
+  * strong scaling (default): the one `size`^3 volume, rank g owns chunk rows [g*n/N, (g+1)*n/N)
+    and holds them plus the 2r halo rows ArraySubsetOverlap would read (array_subset_overlap.rs:
+    11-35), generated on its own device from the global synthetic definition;
+  * weak scaling (`--scaling weak`): a (N*size, size, size) array, each rank owning a size^3 share.
+No data-path collective: the process group carries the barrier and the max over ranks of the timed
+region only. After timing, rank 0 checks a sample of its output chunks (corner, edge, interior)
+against the oracle (oracle/, the reference's per-chunk algorithm) and reports `parity`.
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -26,8 +35,10 @@ EPS = 2500.0
 RADIUS = 4
 N = 2048
 CHUNK = 256
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); measured copy ~6.29 TB/s
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); measured copy ~6.3 TB/s
 ALGO_BYTES_PER_VOXEL = 8  # 4 B compulsory read + 4 B write
+FLOAT_TOL = 1e-5  # |gpu - ref| <= 1e-5 * max(1, |ref|)
+BASELINE_METRIC = "GiB/s filtered (device-resident), guided_filter r=4, 2048³ f32, 256³ chunks"
 
 
 def parse():
@@ -35,43 +46,118 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--size", type=int, default=N, help="per-rank cube edge (default 2048)")
+    ap.add_argument("--size", type=int, default=N,
+                    help="cube edge: the global volume (strong) or each rank's share (weak)")
+    ap.add_argument("--scaling", choices=["strong", "weak"], default="strong")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-chunks", type=int, default=0, help="chunks in the CPU sample")
+    ap.add_argument("--parity-chunks", type=int, default=6,
+                    help="output chunks checked against the oracle after timing (0: skip)")
     ap.add_argument("--radius", type=int, default=RADIUS,
                     help="guided-filter radius (default 4 = the metric; 2 = config G2 at --size 1024)")
     return ap.parse_args()
 
 
-def cpu_baseline(size: int, nchunks: int = 0):
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def maybe_launch(args) -> None:
+    """`--gpus N` outside a launcher: start the N ranks (torch.distributed.run, 127.0.0.1) as a
+    child process before anything touches the GPU, and exit with its status."""
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is not None:
+        if args.gpus != 1 and int(world_env) != args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world_env}", file=sys.stderr)
+            sys.exit(2)
+        return
+    if args.gpus <= 1:
+        return
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+           f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    sys.exit(subprocess.call(cmd, env=env))
+
+
+def cpu_baseline(gshape, radius: int, nchunks: int = 0):
     """Reference algorithm (C restatement of guided_filter.rs, oracle/) on a bounded sample of
-    the same workload: chunks of the same 2048^3 synthetic volume, r=4, 256^3 chunks, each with
-    its 2r halo, all host threads (rayon default), faithful incl. the dead 4th SAT. The default
-    sample, 6 chunks per thread (6 GiB of output), is about 15 s of CPU work at 0.4 GiB/s."""
+    the same workload: chunks of the same synthetic volume, 256^3 chunks, each with its 2r halo,
+    all host threads (rayon default), faithful incl. the dead 4th SAT. The default sample, 6
+    chunks per thread, is about 15 s of CPU work at 0.4 GiB/s."""
     from oracle import oracle as O
     ncpu = os.cpu_count() or 1
     threads = max(1, min(16, ncpu))  # the GPU box grants a 16-CPU share
     nchunks = nchunks or 6 * threads
-    coords = []
-    g = size // CHUNK
-    for i in range(nchunks):  # a diagonal walk through the chunk grid (interior + edge chunks)
-        coords.append(((i * 3) % g, (i * 5 + 1) % g, (i * 7 + 2) % g))
-    secs, vox = O.time_guided_filter_chunks((size,) * 3, (CHUNK,) * 3, coords, EPS, RADIUS,
-                                            threads)
+    grid = [-(-g // CHUNK) for g in gshape]
+    coords = [((i * 3) % grid[0], (i * 5 + 1) % grid[1], (i * 7 + 2) % grid[2])
+              for i in range(nchunks)]  # a diagonal walk through the grid (interior + edges)
+    secs, vox = O.time_guided_filter_chunks(gshape, (CHUNK,) * 3, coords, EPS, radius, threads)
     gibs = vox * 4 / 2 ** 30 / secs
     return {"value": round(gibs, 5), "unit": "GiB/s", "cores": threads, "kind": "port",
-            "sample": f"{nchunks} chunks of 256^3 (r={RADIUS} halo) of the same {size}^3 synthetic "
-                      f"volume, {secs:.2f} s wall on {threads} threads; C restatement of "
-                      f"guided_filter.rs (oracle/zt_oracle.c, faithful incl. dead SAT)"}
+            "sample": f"{nchunks} chunks of 256^3 (r={radius}, 2r halo) of the same "
+                      f"{'x'.join(map(str, gshape))} synthetic volume, {secs:.2f} s wall on "
+                      f"{threads} threads; C restatement of guided_filter.rs "
+                      f"(oracle/zt_oracle.c, faithful incl. dead SAT)"}
 
 
-def load_traffic(size: int):
-    """Per-launch HBM traffic from the committed rocprofv3 PMC summary, if one matches."""
+def parity_sample(out_dev, a, gshape, radius: int, nchunks: int):
+    """Compare a sample of this rank's output chunks (corner, edge, interior) with the oracle's
+    per-chunk result (GuidedFilter::apply_chunk, guided_filter.rs:75-114), outside the timed
+    region."""
+    import numpy as np
+    from oracle import oracle as O
+    grid = [-(-g // CHUNK) for g in gshape]
+    rows = range(a.out_z0 // CHUNK, -(-(a.out_z0 + a.out_nz) // CHUNK))
+    coords = [c for c in O.sample_chunk_coords(grid, n_interior=max(1, nchunks - 4))
+              if c[0] in rows]
+    if not coords:
+        coords = [(rows[0], 0, 0)]
+    for c in O.sample_chunk_coords([len(rows)] + grid[1:]):
+        cc = (rows[0] + c[0],) + tuple(c[1:])
+        if len(coords) >= nchunks:
+            break
+        if cc not in coords:
+            coords.append(cc)
+    coords = coords[:max(nchunks, 1)]
+    threads = max(1, min(16, os.cpu_count() or 1, len(coords)))
+    t0 = time.perf_counter()
+    refs = O.guided_filter_synth_chunks(gshape, (CHUNK,) * 3, coords, EPS, radius, threads)
+    worst, exact, total = 0.0, 0, 0
+    for (o0, osh, ref) in refs:
+        z = o0[0] - a.out_z0
+        got = out_dev[z:z + osh[0], o0[1]:o0[1] + osh[1], o0[2]:o0[2] + osh[2]].cpu().numpy()
+        d = np.abs(got.astype(np.float64) - ref) / np.maximum(1.0, np.abs(ref.astype(np.float64)))
+        worst = max(worst, float(d.max()))
+        exact += int(np.count_nonzero(got == ref))
+        total += got.size
+    return {"max_rel": float(f"{worst:.3e}"), "tol": FLOAT_TOL, "ok": worst <= FLOAT_TOL,
+            "chunks": [list(c) for c in coords], "bit_exact_frac": round(exact / total, 4),
+            "oracle": "oracle/zt_oracle.c per-chunk apply_ndarray on the 2r-halo block",
+            "secs": round(time.perf_counter() - t0, 2)}
+
+
+def lib_hash() -> str:
+    """sha256 of the shipped HIP library: the key a committed PMC traffic profile must match."""
+    h = hashlib.sha256()
+    with open(os.path.join(ROOT, "zarrs_tools_amd", "libzarrs_tools_amd.so"), "rb") as f:
+        for blk in iter(lambda: f.read(1 << 20), b""):
+            h.update(blk)
+    return h.hexdigest()
+
+
+def load_traffic(gshape, radius: int, world: int):
+    """Per-launch HBM traffic from the committed rocprofv3 PMC summary (profiles/pmc_traffic.json),
+    only when it was measured on this exact library build and workload; else None."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
-        if d.get("size") == size and d.get("radius") == RADIUS:
+        if (d.get("lib_sha256") == lib_hash() and list(d.get("global_shape", [])) == list(gshape)
+                and d.get("radius") == radius and d.get("world", 1) == world):
             return d.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass
@@ -79,9 +165,9 @@ def load_traffic(size: int):
 
 
 def main():
-    global RADIUS
     args = parse()
-    RADIUS = args.radius
+    maybe_launch(args)
+    radius = args.radius
     import torch
     import torch.distributed as dist
 
@@ -89,18 +175,19 @@ def main():
     from zarrs_tools_amd import _abi
     from zarrs_tools_amd.filter import _ptr
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    if world_env > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    world = dist.get_world_size() if world_env > 1 else 1  # ranks RCCL actually joined
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
     size = args.size
-    gshape = (size * world, size, size)
-    a = zt.slab_assignment(rank, world, gshape[0], size, 2 * RADIUS)
+    gshape = (size * world, size, size) if args.scaling == "weak" else (size, size, size)
+    a = zt.slab_assignment(rank, world, gshape[0], CHUNK, 2 * radius)
     stream = torch.cuda.current_stream(dev)
     ctx = zt.Context(local, stream)
 
@@ -117,7 +204,7 @@ def main():
     def step():
         _abi.check(L.zt_guided_filter_apply_slab(ctx.handle, 11, _ptr(slab), 11, _ptr(out), gs,
                                                  a.in_z0, a.in_nz, a.out_z0, a.out_nz, cs, EPS,
-                                                 RADIUS))
+                                                 radius))
 
     for _ in range(args.warmup):
         step()
@@ -143,16 +230,19 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         wall, kern_ms = float(tt[0]), float(tt[1])
 
-    voxels_rank = a.out_nz * size * size
-    voxels_all = voxels_rank * world
+    voxels_rank = a.out_nz * size * size  # rank 0's share (the largest, or equal)
+    voxels_all = gshape[0] * size * size
     ms_per_step = wall * 1000.0 / args.steps
     value = voxels_all * 4 / 2 ** 30 / (ms_per_step / 1000.0)
     achieved = voxels_rank * ALGO_BYTES_PER_VOXEL / (kern_ms / 1000.0) / 1e9  # GB/s per GPU
-    traffic = load_traffic(size)
+    traffic = load_traffic(gshape, radius, world)
 
+    headline = (size == N and radius == 4 and args.scaling == "strong") or (
+        world == 1 and size == N and radius == 4)
     res = {
-        "metric": f"GiB/s filtered (device-resident), guided_filter r={RADIUS}, {size}^3 f32, "
-                  f"{CHUNK}^3 chunks",
+        "metric": BASELINE_METRIC if headline else
+        f"GiB/s filtered (device-resident), guided_filter r={radius}, {size}³ f32, "
+        f"{CHUNK}³ chunks",
         "value": round(value, 3),
         "unit": "GiB/s",
         "n_gpus": world,
@@ -160,15 +250,17 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (SURVEY.md §8(d) step+noise, splitmix64 seed 0x5EED2025), generated "
                 "on device",
-        "config": {"workload": f"guided_filter eps={EPS:g} r={RADIUS} on {size}^3 f32 per GPU, "
-                               f"{CHUNK}^3 chunks, device-resident (global array "
-                               f"{gshape[0]}x{size}x{size}, z-slab per rank + 2r halo)",
-                   "chunks_per_gpu": (size // CHUNK) ** 3, "parallelism": f"chunk-rows x{world}"},
+        "config": {"workload": f"guided_filter eps={EPS:g} r={radius} on a "
+                               f"{'x'.join(map(str, gshape))} f32 array, {CHUNK}^3 chunks, "
+                               f"device-resident; rank g owns a z-slab of chunk rows + 2r halo",
+                   "chunks_total": (gshape[0] // CHUNK) * (size // CHUNK) ** 2,
+                   "chunks_rank0": (a.out_nz // CHUNK) * (size // CHUNK) ** 2,
+                   "parallelism": f"chunk-rows x{world} ({args.scaling})"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic,
@@ -177,13 +269,17 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            res["cpu_baseline"] = cpu_baseline(size, args.cpu_chunks)
+            res["cpu_baseline"] = cpu_baseline(gshape, radius, args.cpu_chunks)
         except Exception as e:  # the baseline is reported, never required
             res["cpu_baseline"] = {"value": None, "error": str(e)}
+    if rank == 0 and args.parity_chunks > 0:
+        res["parity"] = parity_sample(out, a, gshape, radius, args.parity_chunks)
+        res["parity_max_rel"] = res["parity"]["max_rel"]
     if rank == 0:
         print(json.dumps(res), flush=True)
     ctx.close()
     if world > 1:
+        dist.barrier()
         dist.destroy_process_group()
 
 

@@ -79,6 +79,11 @@ int zt_ctx_set_stream(zt_ctx* ctx, void* hip_stream);
 int zt_ctx_use_own_stream(zt_ctx* ctx);
 int zt_ctx_get_stream(zt_ctx* ctx, void** hip_stream);
 int zt_ctx_synchronize(zt_ctx* ctx);
+/* Device scratch held by the context between calls (staging casts, separable passes): its size,
+ * and a release that synchronises the stream and frees it (the next call needing scratch
+ * allocates again). Scratch allocation failures return ZT_ERR_OUT_OF_MEMORY. */
+int zt_ctx_scratch_bytes(zt_ctx* ctx, uint64_t* bytes);
+int zt_ctx_release_scratch(zt_ctx* ctx);
 /* Device time in ms of the most recent filter launch recorded on this context (hipEvents around
  * the kernel(s) on the context stream). Valid after zt_ctx_synchronize(). */
 int zt_ctx_last_kernel_ms(zt_ctx* ctx, float* ms);

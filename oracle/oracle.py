@@ -71,6 +71,8 @@ def lib():
         L.oracle_synth_u16.argtypes = [vp, i64p, ctypes.c_int, i64p, ctypes.c_int64,
                                        ctypes.c_uint64]
         L.oracle_synth_block_f32.argtypes = [vp, i64p, i64p, i64p, ctypes.c_uint64]
+        for name in ("oracle_synth_block_nd_f32", "oracle_synth_block_nd_u16"):
+            getattr(L, name).argtypes = [vp, i64p, i64p, i64p, ctypes.c_int, ctypes.c_uint64]
         L.oracle_guided_filter_time_chunks.argtypes = [
             i64p, i64p, i64p, ctypes.c_int, ctypes.c_float, ctypes.c_int, ctypes.c_int,
             ctypes.c_uint64, i64p]
@@ -227,6 +229,68 @@ def synth_block_f32(start, shape, global_shape, seed: int = SEED) -> np.ndarray:
     out = np.empty(tuple(int(s) for s in shape), dtype=np.float32)
     lib().oracle_synth_block_f32(_ptr(out), _shape(start), _shape(shape), _shape(global_shape),
                                  int(seed))
+    return out
+
+
+def synth_block_nd(start, shape, global_shape, kind: str = "float32", seed: int = SEED
+                   ) -> np.ndarray:
+    """The box [start, start+shape) of the N-d global synthetic volume (step+noise f32 or u16
+    noise), equal to the same box of synth_step_noise_f32 / synth_u16 over the whole array."""
+    shape = tuple(int(s) for s in shape)
+    if kind == "float32":
+        out = np.empty(shape, dtype=np.float32)
+        fn = lib().oracle_synth_block_nd_f32
+    else:
+        out = np.empty(shape, dtype=np.uint16)
+        fn = lib().oracle_synth_block_nd_u16
+    fn(_ptr(out), _shape(start), _shape(shape), _shape(global_shape), len(shape), int(seed))
+    return out
+
+
+def chunk_halo_subset(global_shape, chunk_shape, coord, halo):
+    """chunk_subset_bounded + ArraySubsetOverlap::new (guided_filter.rs:87-93,
+    array_subset_overlap.rs:11-35): (output start, output shape, input start, input shape)."""
+    o0 = [c * s for c, s in zip(coord, chunk_shape)]
+    o1 = [min(a + s, g) for a, s, g in zip(o0, chunk_shape, global_shape)]
+    i0 = [max(a - halo, 0) for a in o0]
+    i1 = [min(b + halo, g) for b, g in zip(o1, global_shape)]
+    return (o0, [b - a for a, b in zip(o0, o1)], i0, [b - a for a, b in zip(i0, i1)])
+
+
+def guided_filter_synth_chunks(global_shape, chunk_shape, coords, epsilon: float, radius: int,
+                               nthreads: int = 8, seed: int = SEED):
+    """Expected output of each listed chunk of the synthetic step+noise volume, computed the
+    reference's way (GuidedFilter::apply_chunk, guided_filter.rs:75-114): the 2r-halo input
+    subset clamped to the array, apply_ndarray on it, the halo dropped. Chunks run in parallel
+    threads (ctypes releases the GIL). Returns [(out_start, out_shape, block)]."""
+    from concurrent.futures import ThreadPoolExecutor
+    halo = (2 * int(radius)) & 0xFF
+
+    def one(coord):
+        o0, osh, i0, ish = chunk_halo_subset(global_shape, chunk_shape, coord, halo)
+        blk = synth_block_nd(i0, ish, global_shape, "float32", seed)
+        res = guided_filter_apply_ndarray(blk, epsilon, radius)
+        sl = tuple(slice(a - b, a - b + s) for a, b, s in zip(o0, i0, osh))
+        return (o0, osh, np.ascontiguousarray(res[sl]))
+
+    with ThreadPoolExecutor(max_workers=max(1, nthreads)) as ex:
+        return list(ex.map(one, [tuple(c) for c in coords]))
+
+
+def sample_chunk_coords(grid, n_interior: int = 2):
+    """Corner, edge and interior chunks of a chunk grid: the first and last chunk, one with a
+    single axis at its edge, and n_interior interior chunks (deduplicated)."""
+    nd = len(grid)
+    cs = [tuple(0 for _ in grid), tuple(g - 1 for g in grid)]
+    cs.append(tuple(g // 2 if d else 0 for d, g in enumerate(grid)))           # face chunk
+    cs.append(tuple(g - 1 if d == nd - 1 else g // 2 for d, g in enumerate(grid)))  # x edge
+    for k in range(n_interior):
+        cs.append(tuple(min(max(1, (g * (k + 1)) // (n_interior + 1)), max(g - 2, 0))
+                        for g in grid))
+    out = []
+    for c in cs:
+        if c not in out:
+            out.append(c)
     return out
 
 

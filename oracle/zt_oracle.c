@@ -640,6 +640,41 @@ void oracle_synth_block_f32(float* out, const int64_t* start, const int64_t* sha
             }
 }
 
+/* The box [start, start+shape) of an N-d global synthetic volume (C order), kind 0 = step+noise
+ * f32 (as oracle_synth_step_noise_f32), kind 1 = u16 noise (as oracle_synth_u16): element i of
+ * the box takes the value of its global linear index. Used by the full-size parity samples. */
+static void synth_block_nd(void* out, int kind, const int64_t* start, const int64_t* shape,
+                           const int64_t* global_shape, int ndim, uint64_t seed) {
+    int64_t n = numel(shape, ndim), nx = global_shape[ndim - 1];
+    int64_t idx[16] = {0};
+    for (int64_t i = 0; i < n; ++i) {
+        int64_t gl = 0;
+        for (int d = 0; d < ndim; ++d) gl = gl * global_shape[d] + start[d] + idx[d];
+        uint64_t h = oracle_splitmix64(seed ^ (uint64_t)gl);
+        if (kind == 0) {
+            float U = (float)(h >> 40) * (1.0f / 16777216.0f);
+            float t = 100.0f * U;
+            ((float*)out)[i] = t + (start[ndim - 1] + idx[ndim - 1] >= nx / 2 ? 500.0f : 0.0f);
+        } else {
+            ((uint16_t*)out)[i] = (uint16_t)(((h >> 40) * 65535ull) >> 24);
+        }
+        for (int d = ndim - 1; d >= 0; --d) {
+            if (++idx[d] < shape[d]) break;
+            idx[d] = 0;
+        }
+    }
+}
+
+void oracle_synth_block_nd_f32(float* out, const int64_t* start, const int64_t* shape,
+                               const int64_t* global_shape, int ndim, uint64_t seed) {
+    synth_block_nd(out, 0, start, shape, global_shape, ndim, seed);
+}
+
+void oracle_synth_block_nd_u16(uint16_t* out, const int64_t* start, const int64_t* shape,
+                               const int64_t* global_shape, int ndim, uint64_t seed) {
+    synth_block_nd(out, 1, start, shape, global_shape, ndim, seed);
+}
+
 typedef struct {
     float** blocks;
     int64_t (*shapes)[3];

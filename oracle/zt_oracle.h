@@ -84,6 +84,12 @@ uint64_t oracle_splitmix64(uint64_t x);
  * first axis (for slabs of a larger global volume); shape is the slab's shape, nx = shape[ndim-1]. */
 void oracle_synth_step_noise_f32(float* out, const int64_t* shape, int ndim,
                                  const int64_t* global_shape, int64_t z0, uint64_t seed);
+/* The box [start, start+shape) of an N-d global synthetic volume: step+noise f32 / u16 noise,
+ * element values as the whole-array generators give them (full-size parity samples). */
+void oracle_synth_block_nd_f32(float* out, const int64_t* start, const int64_t* shape,
+                               const int64_t* global_shape, int ndim, uint64_t seed);
+void oracle_synth_block_nd_u16(uint16_t* out, const int64_t* start, const int64_t* shape,
+                               const int64_t* global_shape, int ndim, uint64_t seed);
 /* The box [start, start+shape) of the 3-D global synthetic step+noise volume (C order). */
 void oracle_synth_block_f32(float* out, const int64_t* start, const int64_t* shape,
                             const int64_t* global_shape, uint64_t seed);

@@ -1,0 +1,50 @@
+"""CPU: bench.py's host logic — the post-timing parity sample against the oracle, the
+chunk-row split of the strong-scaled volume, and the --gpus / WORLD_SIZE launcher check."""
+import numpy as np
+import pytest
+import torch
+
+import bench
+from oracle import oracle as O
+import zarrs_tools_amd as zt
+
+
+def test_parity_sample_matches_whole_volume_oracle(monkeypatch):
+    monkeypatch.setattr(bench, "CHUNK", 16)
+    gshape, r = (48, 32, 48), 2
+    v = O.synth_step_noise_f32(gshape)
+    whole = O.guided_filter_apply(v, (16, 16, 16), bench.EPS, r, nthreads=4)
+    for rank in range(2):
+        a = zt.slab_assignment(rank, 2, gshape[0], 16, 2 * r)
+        out = torch.from_numpy(whole[a.out_z0:a.out_z0 + a.out_nz].copy())
+        res = bench.parity_sample(out, a, gshape, r, 4)
+        assert res["ok"] and res["max_rel"] == 0.0 and res["bit_exact_frac"] == 1.0
+        assert all(a.out_z0 // 16 <= c[0] < (a.out_z0 + a.out_nz) // 16 for c in res["chunks"])
+    # a corrupted voxel in a sampled chunk is caught
+    a = zt.slab_assignment(0, 1, gshape[0], 16, 2 * r)
+    bad = torch.from_numpy(whole.copy())
+    bad[0, 0, 0] += 1.0
+    assert not bench.parity_sample(bad, a, gshape, r, 4)["ok"]
+
+
+def test_strong_split_covers_the_volume_once():
+    for world in (1, 2, 4, 8):
+        rows = []
+        for g in range(world):
+            a = zt.slab_assignment(g, world, 2048, 256, 8)
+            rows += list(range(a.out_z0, a.out_z0 + a.out_nz))
+            assert a.in_z0 == max(a.out_z0 - 8, 0)
+            assert a.in_z0 + a.in_nz == min(a.out_z0 + a.out_nz + 8, 2048)
+        assert rows == list(range(2048))
+
+
+def test_gpus_must_match_world_size(monkeypatch):
+    monkeypatch.setenv("WORLD_SIZE", "2")
+
+    class A:
+        gpus = 4
+    with pytest.raises(SystemExit) as e:
+        bench.maybe_launch(A())
+    assert e.value.code == 2
+    A.gpus = 2
+    bench.maybe_launch(A())  # under a launcher with the matching count: no-op

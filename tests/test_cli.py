@@ -75,3 +75,29 @@ def test_ome_factor_rank_mismatch(tmp_path):
     S.create_array(tmp_path / "in", "uint16", (8, 8), (4, 4))
     with pytest.raises(_abi.InvalidParameters):
         ZO.run(str(tmp_path / "in"), str(tmp_path / "out"), factor=[2, 2, 2], log=lambda *a: None)
+
+
+def test_ome_scale_is_input_over_output_shape():
+    # zarrs_ome.rs:570-578: real factor = input / output (integer), accumulated in f32. Extent 3 at
+    # factor 2 -> output 1, factor 3; extent 11 at factor 4 -> output 2, factor 5.
+    s = ZO.level_scale([1.0, 1.0, 1.0], (3, 11, 8), (1, 2, 4))
+    assert s == [3.0, 5.0, 2.0]
+    assert ZO.level_translation(s) == [1.0, 2.0, 0.5]
+    s2 = ZO.level_scale(s, (1, 2, 4), (1, 1, 2))
+    assert s2 == [3.0, 10.0, 4.0]
+
+
+def test_exists_erase_removes_stale_chunks_under_tmp(tmp_path, monkeypatch):
+    # an output under the temp root is erased like any other (prefix test skipped it)
+    out = tmp_path / "out"
+    S.create_array(out, "float32", (4, 4), (2, 2))
+    (out / "c").mkdir(exist_ok=True)
+    (out / "c" / "stale").write_bytes(b"x")
+    calls = []
+    monkeypatch.setattr(S, "guided_filter", lambda *a, **k: calls.append(a) or (_ for _ in ()).throw(
+        _abi.FilterError(_abi.ERR_OTHER, "stop")))
+    S.create_array(tmp_path / "in", "float32", (4, 4), (2, 2))
+    with pytest.raises(_abi.FilterError, match="stop"):
+        ZF.run([{"filter": "guided_filter", "input": str(tmp_path / "in"), "output": str(out),
+                 "epsilon": 1.0, "radius": 1}], tmp=str(tmp_path), log=lambda *a: None)
+    assert calls and not (out / "c" / "stale").exists()

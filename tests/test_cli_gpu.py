@@ -66,3 +66,27 @@ def test_zarrs_ome_levels_and_metadata(tmp_path):
     ms = meta["attributes"]["ome"]["multiscales"][0]
     assert [d["path"] for d in ms["datasets"]] == [str(i) for i in range(7)]
     assert ms["datasets"][1]["coordinateTransformations"][0]["scale"] == [2.0, 2.0, 2.0]
+    # cumulative scale = product of input/output per level (zarrs_ome.rs:570-578): the z axis
+    # goes 5 -> 2 at level 4 (factor 2), 2 -> 1 (2), 1 -> 1 (1); y 9 -> 4 at level 3 (factor 2)
+    shapes = [shape, (20, 18, 35), (10, 9, 17), (5, 4, 8), (2, 2, 4), (1, 1, 2), (1, 1, 1)]
+    sc = [1.0, 1.0, 1.0]
+    for lv in range(1, 7):
+        sc = [a * (i // o) for a, i, o in zip(sc, shapes[lv - 1], shapes[lv])]
+        ct = ms["datasets"][lv]["coordinateTransformations"]
+        assert ct[0]["scale"] == sc
+        assert ct[1]["translation"] == [(a - 1.0) * 0.5 for a in sc]
+
+
+def test_zarrs_ome_extent3_factor2_scale(tmp_path):
+    # extent 3 at factor 2: output 1, real factor 3 (the reference writes 3, not 2)
+    shape, chunk = (3, 8, 12), (2, 4, 4)
+    u = O.synth_u16(shape)
+    S.create_array(tmp_path / "in.zarr", "uint16", shape, chunk)
+    S.write_array(tmp_path / "in.zarr", u)
+    ZO.run(str(tmp_path / "in.zarr"), str(tmp_path / "ome"), max_levels=1, log=lambda *a: None)
+    np.testing.assert_array_equal(S.read_array(tmp_path / "ome" / "1"),
+                                  O.downsample(u, "uint16", (2, 2, 2), "uint16"))
+    meta = json.load(open(tmp_path / "ome" / "zarr.json"))
+    ct = meta["attributes"]["ome"]["multiscales"][0]["datasets"][1]["coordinateTransformations"]
+    assert ct[0]["scale"] == [3.0, 2.0, 2.0]
+    assert ct[1]["translation"] == [1.0, 0.5, 0.5]

@@ -33,7 +33,7 @@
 
 #include <cstdlib>
 
-#include "gf_fused.hpp"
+#include "../zarrs_tools_amd/csrc/gf_fused.hpp"
 
 #ifndef GF_V9_K3
 #define GF_V9_K3 2
@@ -615,7 +615,7 @@ inline bool v9_enabled() {
 }
 
 template <int R, int TY, int NT, typename TIn, typename TOut>
-inline hipError_t launch_fused_auto(const GFParams& p, hipStream_t stream) {
+inline hipError_t launch_fused_auto_v9(const GFParams& p, hipStream_t stream) {
     if constexpr (R >= 1 && R <= 4) {
         if (v9_enabled() && v9_eligible<TIn, TOut>(p, R))
             return launch_v9<R, TIn, TOut>(p, stream);

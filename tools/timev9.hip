@@ -9,7 +9,7 @@
 #include <cstdlib>
 #include <vector>
 
-#include "../zarrs_tools_amd/csrc/gf_v9.hpp"
+#include "gf_v9.hpp"
 
 using namespace zt;
 

@@ -119,6 +119,8 @@ def lib() -> ctypes.CDLL:
         "zt_ctx_get_stream": ([vp, ctypes.POINTER(vp)], c_int),
         "zt_ctx_use_own_stream": ([vp], c_int),
         "zt_ctx_synchronize": ([vp], c_int),
+        "zt_ctx_scratch_bytes": ([vp, ctypes.POINTER(ctypes.c_uint64)], c_int),
+        "zt_ctx_release_scratch": ([vp], c_int),
         "zt_ctx_last_kernel_ms": ([vp, ctypes.POINTER(c_float)], c_int),
         "zt_guided_filter_is_compatible": ([c_int, c_int], c_int),
         "zt_guided_filter_memory_per_chunk": ([c_int, c_int, i64p, c_int,

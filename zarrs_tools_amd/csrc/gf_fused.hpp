@@ -1126,6 +1126,10 @@ inline hipError_t launch_fused_cfg(const GFParams& p0, hipStream_t stream) {
     return e;
 }
 
+template <int R, int TY, int NT, typename TIn, typename TOut>
+inline hipError_t launch_fused_auto(const GFParams& p, hipStream_t stream) {
+    return launch_fused_cfg<R, TY, NT, TIn, TOut>(p, stream);
+}
 
 // Element-type pairs with a direct fused instantiation (the rest are staged through f32).
 inline bool fused_fast_dtype(int d) { return d == kF32 || d == kU16 || d == kU8 || d == kBool; }

@@ -431,14 +431,16 @@ static hipError_t box_all_axes(const T0* src0, T* p0, T* p1, const NdGeom& g, in
 hipError_t launch_guided_separable(const void* in, int dtype_in, void* out, int dtype_out,
                                    const NdGeom& g, int radius, float eps, float* scratch,
                                    hipStream_t s) {
-    // scratch: 5 * numel floats = v (f32) | region X (2n floats) | region Y (2n floats).
+    // scratch: separable_scratch_floats(numel) = v (f32) | region X (2n floats) | region Y (2n
+    // floats), with n padded to a multiple of 4 so X and Y are 16-byte aligned.
     // Stage 1 ping-pongs f64 sums between X and Y; a, b (and their pass ping-pong) then use the
     // region not holding U: A, B in it, A', B' in the other.
     const int64_t n = g.numel;
     if (n <= 0) return hipSuccess;
     float* v = scratch;
-    float* X = scratch + n;
-    float* Y = scratch + 3 * n;
+    const int64_t np = separable_pad(n);
+    float* X = scratch + np;
+    float* Y = scratch + 3 * np;
     const int64_t rows = n / g.shape[g.ndim - 1];
     const unsigned rblocks = (unsigned)std::min<int64_t>(rows, 1 << 20);
     // contiguous f32 input is used in place; anything else is gathered into v

@@ -159,6 +159,25 @@ int dtypes_ok(int dtype_in, int dtype_out) {
     return ZT_OK;
 }
 
+// The fused kernel addresses each z-plane through a buffer descriptor with 32-bit byte offsets
+// (gf_fused.hpp: slice_rsrc, int row strides): every input plane and output plane it touches must
+// span < 2^31 bytes, measured after the f32 staging run_fused3 may insert. Larger planes go to
+// the separable path (64-bit indexing) instead of silently reading zeros past the range.
+bool fused_planes_fit(const int64_t dom[3], int64_t in_sy, const int64_t oshape[3],
+                      int64_t out_sy, int dtype_in, int dtype_out) {
+    const bool stage_in = !zt::fused_direct_pair(dtype_in, zt::kF32);
+    const bool stage_out = !zt::fused_direct_pair(zt::kF32, dtype_out);
+    const int64_t isy = stage_in ? dom[2] : in_sy, osy = stage_out ? oshape[2] : out_sy;
+    const int64_t iesz = stage_in ? 4 : (int64_t)zt::dtype_size(dtype_in);
+    const int64_t oesz = stage_out ? 4 : (int64_t)zt::dtype_size(dtype_out);
+    const int64_t lim = (int64_t)INT32_MAX - 16;  // + one quad of slack past the last element
+    if (dom[1] <= 0 || dom[2] <= 0 || oshape[1] <= 0 || oshape[2] <= 0) return true;
+    const int64_t ib = ((dom[1] - 1) * isy + dom[2]) * iesz;
+    const int64_t ob = ((oshape[1] - 1) * osy + oshape[2]) * oesz;
+    return ib <= lim && ob <= lim && dom[1] <= INT32_MAX && dom[2] <= INT32_MAX &&
+           dom[0] <= INT32_MAX;
+}
+
 // Fused launch on a 3-D view (pad 1-2 D arrays with leading unit axes).
 int run_fused3(zt_ctx* ctx, int dtype_in, const void* in, const int64_t dom[3], int64_t in_z0,
                int64_t in_rows, int64_t in_sz, int64_t in_sy, const int64_t ostart[3],
@@ -167,6 +186,8 @@ int run_fused3(zt_ctx* ctx, int dtype_in, const void* in, const int64_t dom[3], 
     for (int d = 0; d < 3; ++d)
         if (dom[d] > INT32_MAX || oshape[d] > INT32_MAX)
             return fail(ZT_ERR_INVALID_PARAMETERS, "extent exceeds 2^31-1");
+    if (!fused_planes_fit(dom, in_sy, oshape, out_sy, dtype_in, dtype_out))
+        return fail(ZT_ERR_INVALID_PARAMETERS, "fused path: a z-plane spans >= 2 GiB");
     zt::GFParams p{};
     p.in = in;
     p.out = out;
@@ -246,7 +267,7 @@ int run_separable(zt_ctx* ctx, int dtype_in, const void* in, const int64_t* shap
         g.out_strides[d] = out_strides[d];
     }
     if (g.numel == 0 || g.out_numel == 0) return ZT_OK;
-    int rc = ctx->ensure_scratch(sizeof(float) * 5 * (size_t)g.numel);
+    int rc = ctx->ensure_scratch(sizeof(float) * (size_t)zt::separable_scratch_floats(g.numel));
     if (rc) return rc;
     if (ctx->timed) ZT_HIP(hipEventRecord(ctx->ev0, ctx->cur));
     hipError_t e = zt::launch_guided_separable(in, dtype_in, out, dtype_out, g, radius, eps,
@@ -355,6 +376,25 @@ int zt_ctx_synchronize(zt_ctx* ctx) {
     return ZT_OK;
 }
 
+int zt_ctx_scratch_bytes(zt_ctx* ctx, uint64_t* bytes) {
+    if (int rc = check_ctx(ctx)) return rc;
+    if (!bytes) return fail(ZT_ERR_INVALID_PARAMETERS, "null output pointer");
+    *bytes = ctx->scratch_bytes;
+    return ZT_OK;
+}
+
+int zt_ctx_release_scratch(zt_ctx* ctx) {
+    if (int rc = check_ctx(ctx)) return rc;
+    DeviceGuard g(ctx->device);
+    if (ctx->scratch) {
+        ZT_HIP(hipStreamSynchronize(ctx->cur));
+        ZT_HIP(hipFree(ctx->scratch));
+        ctx->scratch = nullptr;
+        ctx->scratch_bytes = 0;
+    }
+    return ZT_OK;
+}
+
 int zt_ctx_last_kernel_ms(zt_ctx* ctx, float* ms) {
     if (int rc = check_ctx(ctx)) return rc;
     if (!ms) return fail(ZT_ERR_INVALID_PARAMETERS, "null output pointer");
@@ -435,8 +475,10 @@ int zt_guided_filter_apply_ndarray(zt_ctx* ctx, int dtype_in, const void* in,
         }
         if (ndim == 3) { isz = is[0]; isy = is[1]; osz = os[0]; osy = os[1]; }
         if (ndim == 2) { isy = is[0]; osy = os[0]; }
-        return run_fused3(ctx, dtype_in, in, dom, 0, dom[0], isz, isy, ost, osh, dtype_out, out,
-                          osz, osy, epsilon, radius, 0);
+        if (ndim == 1) { isy = dom[2]; osy = osh[2]; }
+        if (fused_planes_fit(dom, isy, osh, osy, dtype_in, dtype_out))
+            return run_fused3(ctx, dtype_in, in, dom, 0, dom[0], isz, isy, ost, osh, dtype_out,
+                              out, osz, osy, epsilon, radius, 0);
     }
     return run_separable(ctx, dtype_in, in, in_shape, is, ndim, out_start, out_shape, dtype_out,
                          out, os, epsilon, radius);
@@ -474,7 +516,13 @@ int zt_guided_filter_apply_array(zt_ctx* ctx, int dtype_in, const void* in, int 
     c_strides(shape, ndim, strides);
     DeviceGuard g(ctx->device);
     const size_t esz_in = zt::dtype_size(dtype_in), esz_out = zt::dtype_size(dtype_out);
-    if (ndim <= 3 && zt::fused_supports_radius(radius)) {
+    int64_t fdom[3] = {1, 1, 1}, fosh[3] = {1, 1, 1};
+    for (int d = 0; d < ndim && ndim <= 3; ++d) {
+        fdom[3 - ndim + d] = shape[d];
+        fosh[3 - ndim + d] = oshape[d];
+    }
+    if (ndim <= 3 && zt::fused_supports_radius(radius) &&
+        fused_planes_fit(fdom, fdom[2], fosh, fdom[2], dtype_in, dtype_out)) {
         // One launch for the whole box: every window clamps at the array bounds, which is what
         // the reference's per-chunk 2r halo (clamped to the array) produces.
         int64_t dom[3] = {1, 1, 1}, ost[3] = {0, 0, 0}, osh[3] = {1, 1, 1};
@@ -501,7 +549,8 @@ int zt_guided_filter_apply_array(zt_ctx* ctx, int dtype_in, const void* in, int 
         int rc = zt_subset_overlap(shape, ndim, ostart, oshape, ov, is0, ish, dst);
         if (rc) return rc;
         size_t free_b = 0, total_b = 0;
-        const size_t need = sizeof(float) * 5 * (size_t)numel(ish, ndim);
+        const size_t need =
+            sizeof(float) * (size_t)zt::separable_scratch_floats(numel(ish, ndim));
         const bool have = ctx->scratch_bytes >= need ||
                           (hipMemGetInfo(&free_b, &total_b) == hipSuccess &&
                            need + ctx->scratch_bytes <= free_b / 2);
@@ -569,6 +618,15 @@ int zt_guided_filter_apply_slab(zt_ctx* ctx, int dtype_in, const void* in, int d
     const int64_t sy = global_shape[2], sz = global_shape[1] * global_shape[2];
     int64_t dom[3] = {global_shape[0], global_shape[1], global_shape[2]};
     int64_t ost[3] = {out_z0, 0, 0}, osh[3] = {out_nz, global_shape[1], global_shape[2]};
+    if (!fused_planes_fit(dom, sy, osh, sy, dtype_in, dtype_out)) {
+        // planes of >= 2 GiB: the separable path on the slab block (it carries the 2r halo, so
+        // windows clamped at the block equal windows clamped at the array)
+        const int64_t bsh[3] = {in_nz, global_shape[1], global_shape[2]};
+        const int64_t bst[3] = {sz, sy, 1};
+        const int64_t bos[3] = {out_z0 - in_z0, 0, 0};
+        return run_separable(ctx, dtype_in, in, bsh, bst, 3, bos, osh, dtype_out, out, bst,
+                             epsilon, radius);
+    }
     int depth = chunk_shape && chunk_shape[0] > 0 ? (int)chunk_shape[0] : (int)out_nz;
     return run_fused3(ctx, dtype_in, in, dom, in_z0, in_nz, sz, sy, ost, osh, dtype_out, out, sz,
                       sy, epsilon, radius, depth);

@@ -60,7 +60,10 @@ hipError_t launch_cast_from_f32_3d(const float* in, int dtype, void* out, int64_
                                    int64_t nz, int64_t ny, int64_t nx, hipStream_t s);
 hipError_t launch_guided_fused(const GFParams& p, int dtype_in, int dtype_out, int radius,
                                hipStream_t stream);
-// scratch must hold 5 * g.numel floats
+// scratch must hold separable_scratch_floats(g.numel) floats: v | X (2n) | Y (2n), each region
+// starting on a 16-byte boundary (the f64 / float2 views of X and Y stay aligned for odd n)
+inline int64_t separable_pad(int64_t n) { return (n + 3) & ~(int64_t)3; }
+inline int64_t separable_scratch_floats(int64_t n) { return 5 * separable_pad(n); }
 hipError_t launch_guided_separable(const void* in, int dtype_in, void* out, int dtype_out,
                                    const NdGeom& g, int radius, float eps, float* scratch,
                                    hipStream_t s);

@@ -68,6 +68,15 @@ class Context:
     def synchronize(self) -> None:
         check(lib().zt_ctx_synchronize(self._h))
 
+    def scratch_bytes(self) -> int:
+        n = ctypes.c_uint64()
+        check(lib().zt_ctx_scratch_bytes(self._h, ctypes.byref(n)))
+        return int(n.value)
+
+    def release_scratch(self) -> None:
+        """Free the device scratch the context keeps between calls."""
+        check(lib().zt_ctx_release_scratch(self._h))
+
     def last_kernel_ms(self) -> float:
         ms = ctypes.c_float()
         check(lib().zt_ctx_last_kernel_ms(self._h, ctypes.byref(ms)))

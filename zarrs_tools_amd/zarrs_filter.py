@@ -134,8 +134,10 @@ def run(steps: list, exists: str = "erase", tmp: str | None = None,
             dst = resolve(step.get("output"), "output")
             if exists == "exit" and os.path.exists(os.path.join(dst, "zarr.json")):
                 raise _abi.FilterError(_abi.ERR_OTHER, f"output {dst} already exists")
-            if os.path.isdir(dst) and not dst.startswith(tmp_root):
-                shutil.rmtree(dst)  # create_array erases the output prefix (zarrs_filter.rs:76)
+            if os.path.isdir(dst) and dst not in made:
+                # create_array erases the output prefix (zarrs_filter.rs:76); only the
+                # temporaries this run just made (empty) are kept
+                shutil.rmtree(dst)
             threads = step.get("chunk_limit") or chunk_limit or 0
             info = S.open_array(src)
             if name == "guided_filter":

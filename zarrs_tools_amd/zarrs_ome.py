@@ -26,6 +26,8 @@ import shutil
 import sys
 import time
 
+import numpy as np
+
 from . import _abi
 from . import store as S
 
@@ -47,6 +49,19 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--device", type=int, default=0)
     ap.add_argument("--chunk-limit", type=int, default=0)
     return ap
+
+
+def level_scale(scale, in_shape, out_shape):
+    """relative_scale *= (input / output) as f32 per axis (zarrs_ome.rs:570-578)."""
+    f32 = np.float32
+    return [float(f32(f32(s) * f32(int(i) // int(o)))) for s, i, o in
+            zip(scale, in_shape, out_shape)]
+
+
+def level_translation(scale):
+    """(s - 1.0) * 0.5 in f32 (zarrs_ome.rs:721-723)."""
+    f32 = np.float32
+    return [float(f32(f32(f32(s) - f32(1.0)) * f32(0.5))) for s in scale]
 
 
 def run(input_path, output_path, factor=None, max_levels: int = 10, discrete: bool = False,
@@ -81,7 +96,6 @@ def run(input_path, output_path, factor=None, max_levels: int = 10, discrete: bo
     shape = list(info.shape)
     stats = []
     for i in range(1, max_levels + 1):
-        win = [min(f, s) for f, s in zip(factor, shape)]
         src, dst = os.path.join(output_path, str(i - 1)), os.path.join(output_path, str(i))
         if gauss is not None:
             st = S.downsample_gaussian(src, dst, factor, gauss[0], gauss[1], device=device,
@@ -91,10 +105,12 @@ def run(input_path, output_path, factor=None, max_levels: int = 10, discrete: bo
                               nthreads=nthreads)
         stats.append(st)
         out = S.open_array(dst)
-        scale = [s * w for s, w in zip(scale, win)]
+        # zarrs_ome.rs:570-578: the real factor is input_shape / output_shape (integer division),
+        # accumulated into an f32 scale; translation (s - 1) * 0.5 in f32 (:716-723)
+        scale = level_scale(scale, shape, out.shape)
         datasets.append({"path": str(i), "coordinateTransformations": [
             {"type": "scale", "scale": list(scale)},
-            {"type": "translation", "translation": [(s - 1.0) * 0.5 for s in scale]}]})
+            {"type": "translation", "translation": level_translation(scale)}]})
         log(f"{i}: {list(shape)} -> {list(out.shape)} in {st['wall_s']:.2f}s")
         shape = list(out.shape)
         if all(f == 1 or s == 1 for f, s in zip(factor, shape)):
