@@ -178,9 +178,17 @@ def main():
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # ZT_BENCH_ONE_DEVICE=1 rehearses the N-rank path on a 1-GPU box: every rank on cuda:0, the
+    # barrier / max-reduce over gloo (never used for a reported N>1 number)
+    one_dev = os.environ.get("ZT_BENCH_ONE_DEVICE") == "1"
+    if one_dev:
+        local = 0
     if world_env > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if one_dev:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     world = dist.get_world_size() if world_env > 1 else 1  # ranks RCCL actually joined
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
@@ -226,7 +234,8 @@ def main():
     wall = t1 - t0
     kern_ms = ev0.elapsed_time(ev1) / args.steps  # HIP events on the launch stream
     if world > 1:
-        tt = torch.tensor([wall, kern_ms], dtype=torch.float64, device=dev)
+        tt = torch.tensor([wall, kern_ms], dtype=torch.float64,
+                          device="cpu" if one_dev else dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         wall, kern_ms = float(tt[0]), float(tt[1])
 
@@ -245,7 +254,8 @@ def main():
         f"{CHUNK}³ chunks",
         "value": round(value, 3),
         "unit": "GiB/s",
-        "n_gpus": world,
+        "n_gpus": 1 if one_dev else world,
+        "ranks": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4),

@@ -30,6 +30,18 @@
 #ifndef GF_K4
 #define GF_K4 4  // P4 outputs per thread (row segment of the (a, b) x-window)
 #endif
+#ifndef GF_DIRECT
+#define GF_DIRECT 1  // P3 / P5 load their v values and P5 stores its outputs directly (no Lc /
+                     // Lv5 / Lout LDS staging)
+#endif
+#ifndef GF_NEWTON_A
+#define GF_NEWTON_A 0  // a = s / (s + eps): Markstein's correction on v_rcp_f32 (<= 1 ulp) without
+                       // the Newton step on the reciprocal (a enters only f32 window sums)
+#endif
+#ifndef GF_FASTDIV5
+#define GF_FASTDIV5 1  // stage-2 means as sum * RN(1/count) (one multiply; the sums already
+                       // differ from the reference's f64 SAT sums by a few ulp)
+#endif
 
 namespace zt {
 
@@ -331,14 +343,16 @@ template <> struct Buf<uint8_t> {
 };
 
 // ---- DPP wave shifts of an f64 (lane i <- lane i-1 / i+1; GFX9 wave_shr:1 / wave_shl:1) ----
+// bound_ctrl set: lanes whose source lies outside the wave read 0, so no "old" value has to be
+// materialised in the destination first (update_dpp with old = 0 costs a v_mov per DPP move).
 __device__ __forceinline__ double dpp_from_lower(double v) {
-    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x138, 0xF, 0xF, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x138, 0xF, 0xF, false);
+    const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0x138, 0xF, 0xF, true);
+    const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0x138, 0xF, 0xF, true);
     return __hiloint2double(hi, lo);
 }
 __device__ __forceinline__ double dpp_from_upper(double v) {
-    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x130, 0xF, 0xF, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x130, 0xF, 0xF, false);
+    const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0x130, 0xF, 0xF, true);
+    const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0x130, 0xF, 0xF, true);
     return __hiloint2double(hi, lo);
 }
 
@@ -385,6 +399,14 @@ template <> struct Quad<uint8_t> {
         __builtin_amdgcn_raw_buffer_store_b32(a, r, off, 0, 2);
     }
 };
+
+// Hide a value from the optimiser: keeps `ok ? off : kBadOff` a v_cndmask feeding one
+// unconditional buffer access (otherwise the select becomes an exec-masked branch around two
+// accesses, and the compiler's vmcnt accounting across the branch drains the loads in flight).
+__device__ __forceinline__ int opaque(int v) {
+    __asm__ volatile("" : "+v"(v));
+    return v;
+}
 
 // A quad whose elements may lie partly outside the domain (edge tiles): element e is read at
 // off + e*size when bit e of mask is set, else reads 0 (kBadOff). Interior tiles use Quad::load.
@@ -447,8 +469,8 @@ struct GFConfig {
     static constexpr int SZ_HX = al((E2Y + K3) * PH * 8);
     static constexpr int SZ_LAB = al((E1Y + 1) * PA * 8);
     static constexpr int SZ_HAB = al((E1Y + 1) * PB * 8);
-    static constexpr int SZ_LC = al(E1Y * PC * 4);
-    static constexpr int SZ_T = al(TY * TX * 4);
+    static constexpr int SZ_LC = GF_DIRECT ? 0 : al(E1Y * PC * 4);
+    static constexpr int SZ_T = GF_DIRECT ? 0 : al(TY * TX * 4);
     static constexpr int OFF_HX = 0, OFF_LAB = OFF_HX + SZ_HX, OFF_HAB = OFF_LAB + SZ_LAB;
     static constexpr int OFF_LC = OFF_HAB + SZ_HAB, OFF_LV5 = OFF_LC + SZ_LC;
     static constexpr int OFF_LOUT = OFF_LV5 + SZ_T, OFF_RCP = OFF_LOUT + SZ_T;
@@ -650,6 +672,8 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
 
     // ---- phase bodies ----------------------------------------------------------------------
     float pa[C::NQP1][4], ps[C::NQP1][4];  // P1 inputs for the next stage-1 slice (prefetched)
+    float vc[C::K3];  // GF_DIRECT: v of the next P3 slice at this thread's item (prefetched)
+    float v5[K5];     // GF_DIRECT: v of the next P5 output slice at this thread's outputs
     auto load_p1 = [&](rsrc_t ra, rsrc_t rs) {  // entering slice zc+R, leaving slice zc-R-1
 #pragma unroll
         for (int k = 0; k < C::NQP1; ++k) {
@@ -741,10 +765,12 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
 #pragma unroll
             for (int k = 0; k < NP3; ++k)
                 y[k] = (f2){__builtin_amdgcn_rcpf(den[k].x), __builtin_amdgcn_rcpf(den[k].y)};
+            if constexpr (GF_NEWTON_A) {  // refine 1/den before Markstein's correction
 #pragma unroll
-            for (int k = 0; k < NP3; ++k) e[k] = pk_fma(-den[k], y[k], (f2){1.0f, 1.0f});
+                for (int k = 0; k < NP3; ++k) e[k] = pk_fma(-den[k], y[k], (f2){1.0f, 1.0f});
 #pragma unroll
-            for (int k = 0; k < NP3; ++k) y[k] = pk_fma(e[k], y[k], y[k]);
+                for (int k = 0; k < NP3; ++k) y[k] = pk_fma(e[k], y[k], y[k]);
+            }
 #pragma unroll
             for (int k = 0; k < NP3; ++k) q[k] = sq[k] * y[k];
 #pragma unroll
@@ -771,14 +797,22 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
             else vin[j] = src[j * C::PH];
         }
         slide_sums_f64<R, C::K3>(vin, U);
-        const float* vsrc = Lc + (sg * C::K3) * C::PC + C::XC + col;  // v of slice zc (C1)
         f2* lab = reinterpret_cast<f2*>(Lab);
         f2 Uf[NP3], vv[NP3], fc[NP3], rc[NP3], a[NP3], bb[NP3];
+#if GF_DIRECT
+#pragma unroll
+        for (int k = 0; k < NP3; ++k) {
+            Uf[k] = (f2){(float)U[2 * k], (float)U[2 * k + 1]};
+            vv[k] = (f2){vc[2 * k], vc[2 * k + 1]};  // v of slice zc, loaded a half-step ago
+        }
+#else
+        const float* vsrc = Lc + (sg * C::K3) * C::PC + C::XC + col;  // v of slice zc (C1)
 #pragma unroll
         for (int k = 0; k < NP3; ++k) {
             Uf[k] = (f2){(float)U[2 * k], (float)U[2 * k + 1]};
             vv[k] = (f2){vsrc[(2 * k) * C::PC], vsrc[(2 * k + 1) * C::PC]};
         }
+#endif
         if (xy_interior && zc - R >= 0 && zc + R < nz) {  // wave-uniform: count = W^3
 #pragma unroll
             for (int k = 0; k < NP3; ++k) {
@@ -789,8 +823,9 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
 #pragma unroll
             for (int k = 0; k < NP3; ++k) {
                 const int ey = sg * C::K3 + 2 * k;
-                if (ey < C::E1Y) lab[ey * C::PA + col] = (f2){a[k].x, bb[k].x};
-                if (ey + 1 < C::E1Y) lab[(ey + 1) * C::PA + col] = (f2){a[k].y, bb[k].y};
+                if (ey < C::E1Y) lab[ey * C::PA + col] = __builtin_shufflevector(a[k], bb[k], 0, 2);
+                if (ey + 1 < C::E1Y)
+                    lab[(ey + 1) * C::PA + col] = __builtin_shufflevector(a[k], bb[k], 1, 3);
             }
             return;
         }
@@ -848,6 +883,7 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     // slice, when it is turned into the suffix sum over [P, W) in place; a window ending at
     // position P of block B+1 is suffix_B(P+1) + prefix_{B+1}(P). ~3 packed adds per output
     // instead of an f64 running sum (10 ops).
+    rsrc_t ro5;  // GF_DIRECT: the output slice P5 stores to this step
     auto do_p5 = [&](int tid, int zc, auto slot_c) {  // y-window -> slice sums; z; out -> Lout
         if constexpr (ABL & 8192) return;
         const int col5 = tid % TX, seg5 = tid / TX;
@@ -875,10 +911,15 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
                 for (int j = 0; j < K5; ++j) ring[q][j] = ring[q][j] + ring[q + 1][j];
         }
         const int zo = zc - R;
+#if !GF_DIRECT
         if (zo < zo_begin || zo >= zo_end) return;  // wave-uniform
+#endif
         const int ox = x0 + col5, oyb = y0 + seg5 * K5;
         const bool interior = xy_interior && zo - R >= 0 && zo + R < nz;  // wave-uniform
-        const int cxz = interior ? 0 : clamped_count(ox, nx, R) * clamped_count(zo, nz, R);
+        // (GF_DIRECT: steps that emit nothing run too, their stores dropped by the descriptor;
+        //  the z count is clamped so its table index stays valid there)
+        const int zq = min(max(zo, 0), nz - 1);
+        const int cxz = interior ? 0 : clamped_count(ox, nx, R) * clamped_count(zq, nz, R);
         f2 fc[K5], rc[K5], q[K5], r[K5];
 #pragma unroll
         for (int j = 0; j < K5; ++j) {
@@ -892,19 +933,33 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
                 rc[j] = (f2){rr, rr};
             }
         }
-        // (sum as f32) / (count as f32) for a and b together (exact: Markstein)
+        // (sum as f32) / (count as f32) for a and b together
 #pragma unroll
         for (int j = 0; j < K5; ++j) q[j] = AB[j] * rc[j];
+        if constexpr (!GF_FASTDIV5) {  // correctly rounded (Markstein)
 #pragma unroll
-        for (int j = 0; j < K5; ++j) r[j] = pk_fma(-q[j], fc[j], AB[j]);
+            for (int j = 0; j < K5; ++j) r[j] = pk_fma(-q[j], fc[j], AB[j]);
 #pragma unroll
-        for (int j = 0; j < K5; ++j) q[j] = pk_fma(r[j], rc[j], q[j]);
+            for (int j = 0; j < K5; ++j) q[j] = pk_fma(r[j], rc[j], q[j]);
+        }
+#if GF_DIRECT
+        (void)r;
+#pragma unroll
+        for (int j = 0; j < K5; ++j) {
+            const int oy = oyb + j;
+            const float o = __fadd_rn(__fmul_rn(v5[j], q[j].x), q[j].y);  // v*=ma; v+=mb
+            const int off = (ox < ox_end && oy < oy_end)
+                                ? ((oy - p.oy0) * osy + (ox - p.ox0)) * OSZ : kBadOff;
+            Buf<TOut>::store(from_f32<TOut>(o), ro5, opaque(off));
+        }
+#else
 #pragma unroll
         for (int j = 0; j < K5; ++j) {
             const int ty = seg5 * K5 + j;
             const float v = Lv5[ty * TX + col5];                  // v of slice zo (staged in C1)
             Lout[ty * TX + col5] = __fadd_rn(__fmul_rn(v, q[j].x), q[j].y);  // v*=ma; v+=mb
         }
+#endif
     };
 
     // ---- C1 staging: 16-byte quads between global memory and the LDS tiles ------------------
@@ -930,6 +985,31 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
             quad_t(q, ox, oy, mask);
             const int off = (EDGE ? q >= 0 : mask == 0xF) ? (oy * sy + ox) * ESZ : kBadOff;
             load_quad(r, off, mask, vq4);
+        }
+    };
+    // GF_DIRECT loaders: one element per access, lanes on consecutive x (coalesced rows).
+    // Positions outside the domain either read 0 through the range check or read a neighbour
+    // row's value that is never used (P3 zeroes its out-of-domain (a, b); P5's store drops).
+    auto load_p3v = [&](rsrc_t r) {
+        const int item = (int)threadIdx.x - C::T3;
+        const int col = item % C::E1X, sg = item / C::E1X;
+        const int gx = x0 - R + col, gy0 = y0 - R + sg * C::K3;
+#pragma unroll
+        for (int k = 0; k < C::K3; ++k) {
+            const int gy = gy0 + k;
+            bool ok = item >= 0;
+            if constexpr (EDGE) ok = ok && (unsigned)gx < (unsigned)nx && (unsigned)gy < (unsigned)ny;
+            vc[k] = Buf<TIn>::load(r, opaque(ok ? (gy * sy + gx) * ESZ : kBadOff));
+        }
+    };
+    auto load_p5v = [&](rsrc_t r) {
+        const int col5 = (int)threadIdx.x % TX, seg5 = (int)threadIdx.x / TX;
+        const int ox = x0 + col5, oyb = y0 + seg5 * K5;
+#pragma unroll
+        for (int j = 0; j < K5; ++j) {
+            const int oy = oyb + j;
+            const bool ok = ox < ox_end && oy < oy_end;
+            v5[j] = Buf<TIn>::load(r, opaque(ok ? (oy * sy + ox) * ESZ : kBadOff));
         }
     };
     float* const dummy = reinterpret_cast<float*>(smem + C::OFF_DUMMY);  // inactive lanes' writes
@@ -959,11 +1039,16 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
 
     // ---- prologue: stage 1 of the first slice up to Hx, first Lc; prefetch step 1 -----------
     load_p1(slice_rsrc(zc_begin + R), slice_rsrc(zc_begin - R - 1));
+#if GF_DIRECT
+    load_p3v(slice_rsrc(zc_begin));
+    do_p12(tid0);
+#else
     load_c(slice_rsrc(zc_begin));
     do_p12(tid0);
     write_c(tid0);
     load_c(slice_rsrc(zc_begin + 1));
     load_v5(slice_rsrc(zc_begin - R));
+#endif
     load_p1(slice_rsrc(zc_begin + 1 + R), slice_rsrc(zc_begin - R));
     lds_barrier_abl<ABL>();
 
@@ -1004,6 +1089,9 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
                             __builtin_amdgcn_s_memtime();
                 }
             };
+#if GF_DIRECT
+            ro5 = make_rsrc(out_base + os, (unsigned)(zs - zo_begin) < nzo ? oslice_bytes : 0u);
+#endif
             stamp(0);
             // Fair progress across the waves of a SIMD: the hardware issues oldest-first, which
             // staggers the waves so the youngest runs its last phase alone, latency exposed. A
@@ -1018,7 +1106,11 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
                 do_p3(tid, i);
                 if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(1);
                 stamp(4);
-                if (i > zc_begin) do_p5(tid, i - 1, std::integral_constant<int, (k + W - 1) % W>{});
+                // GF_DIRECT: unconditional, so no branch separates P5's stores from the loads
+                // waited on later (the first call's slice lies in no emitted window, and its
+                // stores go to a zero-record descriptor)
+                if (GF_DIRECT || i > zc_begin)
+                    do_p5(tid, i - 1, std::integral_constant<int, (k + W - 1) % W>{});
             }
             stamp(1);
             lds_barrier_abl<ABL>();
@@ -1026,12 +1118,18 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
             if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(3);
             // C1: staging (store out(i-1-R), Lc <- slice i+1, Lv5 <- slice i-R), the loads of
             // the next step, P12(i+1), P4(i). Every wait here is for a load issued a step ago.
+#if GF_DIRECT
+            // next step's P3 slice i+1 (= zb + R) and P5 slice i-R (= zb - 1)
+            load_p3v(rs_in(ob + (int64_t)R * sstride, zb + R));
+            load_p5v(rs_in(ob - sstride, zb - 1));
+#else
             store_out(tid, make_rsrc(out_base + os,
                                      (unsigned)(zs - zo_begin) < nzo ? oslice_bytes : 0u));
             write_c(tid);
             write_v5(tid);
             load_c(rs_in(ob + off_c, zb + R + 1));
             load_v5(r_b);
+#endif
             stamp(6);
             if constexpr (GF_PRIO >= 2) __builtin_amdgcn_s_setprio(2);
             if constexpr (GF_ORDER & 2) do_p4(tid);

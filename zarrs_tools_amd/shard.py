@@ -38,3 +38,104 @@ def slab_assignment(rank: int, world: int, n_rows: int, chunk_rows: int, halo: i
     if z1 <= z0:
         i0 = i1 = z0
     return SlabAssignment(rank, world, c0, c1, z0, z1 - z0, i0, i1 - i0)
+
+
+# ---- zarrs_ome pyramid: octant ownership ------------------------------------
+#
+# The reference computes level i from level i-1 chunk by chunk (zarrs_ome.rs:515-738). Across GPUs
+# the level-0 array is split into boxes whose boundaries are multiples of factor^L (L = the number
+# of levels), so every level's downsample windows (exact_chunks, downsample.rs:72-97) stay inside
+# one box: each rank computes all L levels of its box locally, with no exchange, and the union of
+# the ranks' levels is the global pyramid. Output chunks that span several boxes (the upper levels,
+# smaller than a chunk per rank) are assembled on the host from the ranks' sub-blocks
+# (assemble_chunk) before they are encoded.
+
+
+def pyramid_level_shapes(shape, factor, max_levels: int) -> list:
+    """Level shapes and stop rule of zarrs_ome.rs:515-560, :731-737 (output = max(n / f, 1))."""
+    cur, out = list(shape), []
+    for _ in range(max_levels):
+        nxt = [max(s // f, 1) for s, f in zip(cur, factor)]
+        out.append(tuple(nxt))
+        cur = nxt
+        if all(f == 1 or s == 1 for f, s in zip(factor, nxt)):
+            break
+    return out
+
+
+@dataclass(frozen=True)
+class OctantAssignment:
+    rank: int
+    world: int
+    grid: tuple          # ranks per axis
+    coord: tuple         # this rank's position in the rank grid
+    start: tuple         # level-0 box start (multiple of factor^L per axis)
+    shape: tuple         # level-0 box shape
+    level_boxes: tuple   # ((start, shape) of the owned box of level k) for k = 1..L
+
+
+def _rank_grid(world: int, units) -> tuple:
+    """Factor `world` over the axes, each prime factor to the axis with the most aligned units
+    per rank (ties: the slowest axis), never splitting an axis below one unit per rank."""
+    grid = [1] * len(units)
+    n, p, primes = world, 2, []
+    while n > 1:
+        while n % p == 0:
+            primes.append(p)
+            n //= p
+        p += 1
+    for p in sorted(primes, reverse=True):
+        best = max(range(len(units)), key=lambda d: (units[d] // (grid[d] * p) >= 1,
+                                                      units[d] / grid[d], -d))
+        if units[best] // (grid[best] * p) < 1:
+            raise ValueError(f"cannot split {list(units)} aligned units over {world} ranks")
+        grid[best] *= p
+    return tuple(grid)
+
+
+def octant_assignment(rank: int, world: int, shape, factor, max_levels: int) -> OctantAssignment:
+    """The level-0 box rank `rank` of `world` owns and its box at every pyramid level."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError("bad rank/world")
+    levels = pyramid_level_shapes(shape, factor, max_levels)
+    L = len(levels)
+    align = [f ** L for f in factor]
+    units = [s // a for s, a in zip(shape, align)]
+    grid = _rank_grid(world, units)
+    coord, r = [], rank
+    for g in reversed(grid):
+        coord.append(r % g)
+        r //= g
+    coord = tuple(reversed(coord))
+    start, end = [], []
+    for d, (g, c) in enumerate(zip(grid, coord)):
+        u0, u1 = c * units[d] // g, (c + 1) * units[d] // g
+        start.append(u0 * align[d])
+        end.append(shape[d] if c == g - 1 else u1 * align[d])
+    boxes = []
+    for k in range(1, L + 1):
+        fk = [f ** k for f in factor]
+        s_k = [a // f for a, f in zip(start, fk)]
+        e_k = [levels[k - 1][d] if coord[d] == grid[d] - 1 else end[d] // fk[d]
+               for d in range(len(shape))]
+        boxes.append((tuple(s_k), tuple(b - a for a, b in zip(s_k, e_k))))
+    return OctantAssignment(rank, world, grid, coord, tuple(start),
+                            tuple(b - a for a, b in zip(start, end)), tuple(boxes))
+
+
+def assemble_chunk(chunk_start, chunk_shape, pieces):
+    """Host gather of one output chunk from the ranks' sub-blocks of a level: `pieces` is a list
+    of (box_start, array) in the level's coordinates; each contributes its intersection."""
+    import numpy as np
+    out = None
+    for bstart, arr in pieces:
+        lo = [max(c, b) for c, b in zip(chunk_start, bstart)]
+        hi = [min(c + s, b + n) for c, s, b, n in zip(chunk_start, chunk_shape, bstart, arr.shape)]
+        if any(h <= l for l, h in zip(lo, hi)):
+            continue
+        if out is None:
+            out = np.zeros(tuple(chunk_shape), dtype=arr.dtype)
+        dst = tuple(slice(l - c, h - c) for l, h, c in zip(lo, hi, chunk_start))
+        src = tuple(slice(l - b, h - b) for l, h, b in zip(lo, hi, bstart))
+        out[dst] = arr[src]
+    return out
