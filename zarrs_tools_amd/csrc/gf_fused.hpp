@@ -34,6 +34,23 @@
 #define GF_DIRECT 1  // P3 / P5 load their v values and P5 stores its outputs directly (no Lc /
                      // Lv5 / Lout LDS staging)
 #endif
+#ifndef GF_ONEBAR
+#define GF_ONEBAR 0  // (measured slower: 34.4 vs 32.6 ms) one barrier per z-step: every wave runs P12(i+1), P5(i-2), P3(i), P4(i-1)
+                     // on double-buffered Hx / Lab / Hab (when they fit the LDS; needs GF_DIRECT)
+#endif
+#ifndef GF_OCT
+#define GF_OCT 0  // 8 x per P12 lane: fewer instructions, but concentrated on half the waves
+                  // (measured slower: 35.0 vs 31.7 ms)
+#endif
+#ifndef GF_P3_SPREAD
+#define GF_P3_SPREAD 0  // measured slower (34.1 vs 31.8 ms): the extra issue outweighs the balance
+#endif
+#ifndef GF_V5_AUX
+#define GF_V5_AUX 0  // cache policy of P5's v loads (the last read of an input slice)
+#endif
+#ifndef GF_LEAVE_AUX
+#define GF_LEAVE_AUX 0  // cache policy of P1's leaving-slice loads
+#endif
 #ifndef GF_NEWTON_A
 #define GF_NEWTON_A 0  // a = s / (s + eps): Markstein's correction on v_rcp_f32 (<= 1 ulp) without
                        // the Newton step on the reciprocal (a enters only f32 window sums)
@@ -316,8 +333,9 @@ __device__ __forceinline__ rsrc_t make_rsrc(const void* base, uint32_t bytes) {
 
 template <typename T> struct Buf;
 template <> struct Buf<float> {
+    template <int AUX = 0>
     __device__ static float load(rsrc_t r, int off) {
-        return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+        return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, AUX));
     }
     // Output stores are streamed with the non-temporal hint (aux 2 = nt) so they do not evict
     // the input slices the march re-reads from L2 a few steps later.
@@ -326,16 +344,18 @@ template <> struct Buf<float> {
     }
 };
 template <> struct Buf<uint16_t> {
+    template <int AUX = 0>
     __device__ static float load(rsrc_t r, int off) {
-        return (float)(uint16_t)__builtin_amdgcn_raw_buffer_load_b16(r, off, 0, 0);
+        return (float)(uint16_t)__builtin_amdgcn_raw_buffer_load_b16(r, off, 0, AUX);
     }
     __device__ static void store(uint16_t v, rsrc_t r, int off) {
         __builtin_amdgcn_raw_buffer_store_b16(v, r, off, 0, 2);
     }
 };
 template <> struct Buf<uint8_t> {
+    template <int AUX = 0>
     __device__ static float load(rsrc_t r, int off) {
-        return (float)(uint8_t)__builtin_amdgcn_raw_buffer_load_b8(r, off, 0, 0);
+        return (float)(uint8_t)__builtin_amdgcn_raw_buffer_load_b8(r, off, 0, AUX);
     }
     __device__ static void store(uint8_t v, rsrc_t r, int off) {
         __builtin_amdgcn_raw_buffer_store_b8(v, r, off, 0, 2);
@@ -362,8 +382,9 @@ typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
 template <typename T> struct Quad;
 template <> struct Quad<float> {
+    template <int AUX = 0>
     __device__ static void load(rsrc_t r, int off, float (&v)[4]) {
-        const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+        const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, AUX);
         // (not __builtin_bit_cast on q.y: clang reads element 0 for a bit_cast of a vector
         //  element lvalue)
         v[0] = __uint_as_float(q.x); v[1] = __uint_as_float(q.y);
@@ -376,8 +397,9 @@ template <> struct Quad<float> {
     }
 };
 template <> struct Quad<uint16_t> {
+    template <int AUX = 0>
     __device__ static void load(rsrc_t r, int off, float (&v)[4]) {
-        const u32x2 q = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+        const u32x2 q = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, AUX);
         v[0] = (float)(q.x & 0xffffu); v[1] = (float)(q.x >> 16);
         v[2] = (float)(q.y & 0xffffu); v[3] = (float)(q.y >> 16);
     }
@@ -388,8 +410,9 @@ template <> struct Quad<uint16_t> {
     }
 };
 template <> struct Quad<uint8_t> {
+    template <int AUX = 0>
     __device__ static void load(rsrc_t r, int off, float (&v)[4]) {
-        const uint32_t q = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
+        const uint32_t q = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, AUX);
         v[0] = (float)(q & 0xffu); v[1] = (float)((q >> 8) & 0xffu);
         v[2] = (float)((q >> 16) & 0xffu); v[3] = (float)(q >> 24);
     }
@@ -455,11 +478,17 @@ struct GFConfig {
     static constexpr int N3 = E1X * S3, N4 = E1Y * S4;  // work items
     // P12: one lane per quad (4 consecutive x) of an E2 row, whole rows per wave, so the
     // x-neighbour quads of the window sums come from adjacent lanes (DPP), never across waves
-    static constexpr int NQ1X = E2X / 4;                   // quads per E2 row
+    // GF_OCT: 8 consecutive x per lane (two quads) where E2 rows are whole octets: half the
+    // DPP moves and fewer sliding-sum adds per x-sum output
+    static constexpr int QPL = (GF_OCT && E2X % 8 == 0 && R <= 8) ? 2 : 1;  // quads per lane
+    static constexpr int EPL = 4 * QPL;                    // elements per lane
+    static constexpr int NQ1X = E2X / EPL;                 // lanes per E2 row
     static constexpr int RPW = 64 / NQ1X;                  // E2 rows per wave
     static constexpr int NWAVE = NT / 64;
     static constexpr int NQP1 = (E2Y + RPW * NWAVE - 1) / (RPW * NWAVE);  // passes
-    static constexpr int NB = (R + 3) / 4;                 // neighbour quads on each side
+    // single pass: P12 rows on the top waves (P4 works on the bottom ones)
+    static constexpr int W12 = NQP1 == 1 ? NWAVE - (E2Y + RPW - 1) / RPW : 0;
+    static constexpr int NB = (R + EPL - 1) / EPL;         // neighbour lanes on each side
     static constexpr int XC = R % 4;  // Lc quad grid starts XC elements left of the E1 apron
     static constexpr int NQCX = (E1X + XC + 3) / 4, NQC = NQCX * E1Y;  // Lc: the E1 apron
     static constexpr int PC = 4 * NQCX;                      // Lc pitch (floats)
@@ -471,10 +500,15 @@ struct GFConfig {
     static constexpr int SZ_HAB = al((E1Y + 1) * PB * 8);
     static constexpr int SZ_LC = GF_DIRECT ? 0 : al(E1Y * PC * 4);
     static constexpr int SZ_T = GF_DIRECT ? 0 : al(TY * TX * 4);
-    static constexpr int OFF_HX = 0, OFF_LAB = OFF_HX + SZ_HX, OFF_HAB = OFF_LAB + SZ_LAB;
-    static constexpr int OFF_LC = OFF_HAB + SZ_HAB, OFF_LV5 = OFF_LC + SZ_LC;
-    static constexpr int OFF_LOUT = OFF_LV5 + SZ_T, OFF_RCP = OFF_LOUT + SZ_T;
     static constexpr int SZ_RCP = al((W3 + 1) * 4);  // RN(1/c) for window counts c <= W^3
+    // single-barrier pipeline: Hx / Lab / Hab double-buffered by step parity, if they fit
+    static constexpr bool ONEBAR = GF_ONEBAR && GF_DIRECT &&
+                                   2 * (SZ_HX + SZ_LAB + SZ_HAB) + SZ_RCP + 256 <= 160 * 1024;
+    static constexpr int NBUF = ONEBAR ? 2 : 1;
+    static constexpr int OFF_HX = 0, OFF_LAB = OFF_HX + NBUF * SZ_HX;
+    static constexpr int OFF_HAB = OFF_LAB + NBUF * SZ_LAB;
+    static constexpr int OFF_LC = OFF_HAB + NBUF * SZ_HAB, OFF_LV5 = OFF_LC + SZ_LC;
+    static constexpr int OFF_LOUT = OFF_LV5 + SZ_T, OFF_RCP = OFF_LOUT + SZ_T;
     static constexpr int OFF_DUMMY = OFF_RCP + SZ_RCP;  // 16-B sink for inactive lanes' writes
     static constexpr int LDS_BYTES = OFF_DUMMY + 256;
     // item -> thread placement: heavy phases on different waves (see C0 / C1)
@@ -486,6 +520,7 @@ struct GFConfig {
     static_assert(RPW >= 1, "an E2 row fits one wave");
     static_assert(NQC <= NT && NQ5 <= NT, "one staging quad per thread");
     static_assert(E2X % 4 == 0, "E2 rows are whole quads");
+    static_assert(E2X % EPL == 0, "E2 rows are whole lane items");
     static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 };
 
@@ -503,9 +538,19 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     constexpr int K5 = C::K5;
     constexpr int ESZ = (int)sizeof(TIn), OSZ = (int)sizeof(TOut);
     extern __shared__ __attribute__((aligned(16))) char smem[];
+    // (re-pointed at the buffer of the step's parity before each phase when C::ONEBAR)
     double* Hx = reinterpret_cast<double*>(smem + C::OFF_HX);
     float2* Lab = reinterpret_cast<float2*>(smem + C::OFF_LAB);
     float2* Hab = reinterpret_cast<float2*>(smem + C::OFF_HAB);
+    auto set_hx = [&](int i) {
+        Hx = reinterpret_cast<double*>(smem + C::OFF_HX + (i & 1) * C::SZ_HX);
+    };
+    auto set_lab = [&](int i) {
+        Lab = reinterpret_cast<float2*>(smem + C::OFF_LAB + (i & 1) * C::SZ_LAB);
+    };
+    auto set_hab = [&](int i) {
+        Hab = reinterpret_cast<float2*>(smem + C::OFF_HAB + (i & 1) * C::SZ_HAB);
+    };
     float* Lc = reinterpret_cast<float*>(smem + C::OFF_LC);
     float* Lv5 = reinterpret_cast<float*>(smem + C::OFF_LV5);
     float* Lout = reinterpret_cast<float*>(smem + C::OFF_LOUT);
@@ -587,26 +632,30 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
 
     // ---- per-thread, step-invariant quad offsets and in-domain masks -----------------------
     const int tid0 = threadIdx.x;
-    int q1off[C::NQP1], q1mask[C::NQP1];
-    // P12 lane -> (E2 row, quad) for pass k
+    constexpr int QPL = C::QPL, EPL = C::EPL;
+    int q1off[C::NQP1][QPL], q1mask[C::NQP1][QPL];
+    // P12 lane -> (E2 row, lane item = EPL consecutive x) for pass k
     auto p12_pos = [&](int tid, int k, int& row, int& cq) -> bool {
-        const int w = tid / 64, l = tid % 64;
+        const int w = tid / 64 - C::W12, l = tid % 64;
         row = (k * C::NWAVE + w) * C::RPW + l / C::NQ1X;
         cq = l % C::NQ1X;
-        return l < C::RPW * C::NQ1X && row < C::E2Y;
+        return w >= 0 && l < C::RPW * C::NQ1X && row < C::E2Y;
     };
 #pragma unroll
     for (int k = 0; k < C::NQP1; ++k) {
         int row, cq;
         const bool valid = p12_pos(tid0, k, row, cq);
-        const int gx = x0 - 2 * R + 4 * cq, gy = y0 - 2 * R + row;
-        int m = 0;
-        if (valid && gy >= 0 && gy < ny) {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) m |= (gx + e >= 0 && gx + e < nx) ? (1 << e) : 0;
+        for (int h = 0; h < QPL; ++h) {
+            const int gx = x0 - 2 * R + EPL * cq + 4 * h, gy = y0 - 2 * R + row;
+            int m = 0;
+            if (valid && gy >= 0 && gy < ny) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) m |= (gx + e >= 0 && gx + e < nx) ? (1 << e) : 0;
+            }
+            q1mask[k][h] = m;
+            q1off[k][h] = (EDGE ? valid : m == 0xF) ? (gy * sy + gx) * ESZ : kBadOff;
         }
-        q1mask[k] = m;
-        q1off[k] = (EDGE ? valid : m == 0xF) ? (gy * sy + gx) * ESZ : kBadOff;
     }
     // Lc / v5 / output quads: offsets and masks are recomputed at their one use per step
     // (a few integer ops) rather than held in registers across the march.
@@ -640,11 +689,11 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
         else Quad<TIn>::load(r, off, v);
     };
 
-    double zv[C::NQP1][4];
+    double zv[C::NQP1][EPL];
 #pragma unroll
     for (int k = 0; k < C::NQP1; ++k)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) zv[k][e] = 0.0;
+        for (int e = 0; e < EPL; ++e) zv[k][e] = 0.0;
     // Running z-window: seed Zv(zc_begin - 1) = sum of v over [zc_begin-1-R, zc_begin-1+R]
     // clamped to [0, nz); every later step adds the entering and subtracts the leaving slice
     // (both 0 outside the domain), so the window stays exact through out-of-domain steps.
@@ -653,12 +702,14 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
         for (int z = za; z <= zb_; ++z) {
             const rsrc_t rs = slice_rsrc(z);
 #pragma unroll
-            for (int k = 0; k < C::NQP1; ++k) {
-                float v[4];
-                load_quad(rs, q1off[k], q1mask[k], v);
+            for (int k = 0; k < C::NQP1; ++k)
 #pragma unroll
-                for (int e = 0; e < 4; ++e) zv[k][e] += (double)v[e];
-            }
+                for (int h = 0; h < QPL; ++h) {
+                    float v[4];
+                    load_quad(rs, q1off[k][h], q1mask[k][h], v);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) zv[k][4 * h + e] += (double)v[e];
+                }
         }
     }
 
@@ -670,18 +721,42 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
 #pragma unroll
     for (int j = 0; j < K5; ++j) pre[j] = (f2){0.0f, 0.0f};
 
+    // P3 item of a thread (-1: none). GF_P3_SPREAD: the items spread evenly over all waves
+    // (every wave carries the same P3 work, so no SIMD finishes its share late), else the top
+    // N3 threads.
+    auto p3_item = [&](int tid) -> int {
+        if constexpr (GF_P3_SPREAD) {
+            constexpr int per = (C::N3 + C::NWAVE - 1) / C::NWAVE;
+            const int l = tid % 64, it = (tid / 64) * per + l;
+            return (l < per && it < C::N3) ? it : -1;
+        } else {
+            return tid - C::T3;
+        }
+    };
     // ---- phase bodies ----------------------------------------------------------------------
-    float pa[C::NQP1][4], ps[C::NQP1][4];  // P1 inputs for the next stage-1 slice (prefetched)
+    float pa[C::NQP1][EPL], ps[C::NQP1][EPL];  // P1 inputs of the next stage-1 slice (prefetched)
     float vc[C::K3];  // GF_DIRECT: v of the next P3 slice at this thread's item (prefetched)
     float v5[K5];     // GF_DIRECT: v of the next P5 output slice at this thread's outputs
+#pragma unroll
+    for (int j = 0; j < K5; ++j) v5[j] = 0.0f;
     auto load_p1 = [&](rsrc_t ra, rsrc_t rs) {  // entering slice zc+R, leaving slice zc-R-1
 #pragma unroll
-        for (int k = 0; k < C::NQP1; ++k) {
-            if constexpr (ABL & 8) { for (int e = 0; e < 4; ++e) pa[k][e] = 1.0f; }
-            else load_quad(ra, q1off[k], q1mask[k], pa[k]);
-            if constexpr (ABL & 1) { for (int e = 0; e < 4; ++e) ps[k][e] = 0.5f; }
-            else load_quad(rs, q1off[k], q1mask[k], ps[k]);
-        }
+        for (int k = 0; k < C::NQP1; ++k)
+#pragma unroll
+            for (int h = 0; h < QPL; ++h) {
+                float a4[4], s4[4];
+                if constexpr (ABL & 8) { for (int e = 0; e < 4; ++e) a4[e] = 1.0f; }
+                else load_quad(ra, q1off[k][h], q1mask[k][h], a4);
+                if constexpr (ABL & 1) { for (int e = 0; e < 4; ++e) s4[e] = 0.5f; }
+                else if constexpr (!EDGE && GF_LEAVE_AUX != 0)
+                    Quad<TIn>::template load<GF_LEAVE_AUX>(rs, q1off[k][h], s4);
+                else load_quad(rs, q1off[k][h], q1mask[k][h], s4);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    pa[k][4 * h + e] = a4[e];
+                    ps[k][4 * h + e] = s4[e];
+                }
+            }
     };
     // P12: z-window of v (f64, running) and its x-window sums on the E2 apron -> Hx. The x
     // neighbours come from the adjacent lanes' quads by DPP wave shifts (whole rows per wave),
@@ -693,45 +768,45 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
             int row, cq;
             const bool valid = p12_pos(tid, k, row, cq);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
+            for (int e = 0; e < EPL; ++e) {
                 zv[k][e] = zv[k][e] + (double)pa[k][e];  // entering slice (0 outside the domain)
                 zv[k][e] = zv[k][e] - (double)ps[k][e];  // leaving slice (0 outside the domain)
             }
             constexpr int NB = C::NB;
-            double win[4 * (2 * NB + 1)];  // quads q-NB .. q+NB
+            double win[EPL * (2 * NB + 1)];  // lane items cq-NB .. cq+NB
 #pragma unroll
-            for (int e = 0; e < 4; ++e) win[4 * NB + e] = zv[k][e];
+            for (int e = 0; e < EPL; ++e) win[EPL * NB + e] = zv[k][e];
+            // only the R elements next to the own item are read (the others' moves are dead)
 #pragma unroll
             for (int n = 1; n <= NB; ++n)
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
+                for (int e = 0; e < EPL; ++e) {
                     if constexpr (ABL & 512) {
-                        win[4 * (NB - n) + e] = win[4 * (NB - n + 1) + e] * 0.5;
-                        win[4 * (NB + n) + e] = win[4 * (NB + n - 1) + e] * 0.25;
+                        win[EPL * (NB - n) + e] = win[EPL * (NB - n + 1) + e] * 0.5;
+                        win[EPL * (NB + n) + e] = win[EPL * (NB + n - 1) + e] * 0.25;
                     } else {
-                        win[4 * (NB - n) + e] = dpp_from_lower(win[4 * (NB - n + 1) + e]);
-                        win[4 * (NB + n) + e] = dpp_from_upper(win[4 * (NB + n - 1) + e]);
+                        win[EPL * (NB - n) + e] = dpp_from_lower(win[EPL * (NB - n + 1) + e]);
+                        win[EPL * (NB + n) + e] = dpp_from_upper(win[EPL * (NB + n - 1) + e]);
                     }
                 }
-            double vin[4 + 2 * R], hs[4];
+            double vin[EPL + 2 * R], hs[EPL];
 #pragma unroll
-            for (int j = 0; j < 4 + 2 * R; ++j) vin[j] = win[4 * NB - R + j];
-            slide_sums_f64<R, 4>(vin, hs);
+            for (int j = 0; j < EPL + 2 * R; ++j) vin[j] = win[EPL * NB - R + j];
+            slide_sums_f64<R, EPL>(vin, hs);
             if constexpr (GF_HX_B128 && R % 2 == 0) {
-                // even R: the quad's outputs land on two 16-byte aligned column pairs of Hx
-                // (E1X and the pitch are even): two b128 writes per lane instead of four b64
-                // ones (lanes 32 B apart: a 4-way bank conflict per b64 write)
+                // even R: the item's outputs land on 16-byte aligned column pairs of Hx (E1X and
+                // the pitch are even): b128 writes (b64 writes of lanes 32 B apart conflict)
 #pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const int colh = 4 * cq + 2 * h - R;
+                for (int h = 0; h < EPL / 2; ++h) {
+                    const int colh = EPL * cq + 2 * h - R;
                     if (valid && colh >= 0 && colh + 1 < C::E1X)
                         *reinterpret_cast<double2*>(Hx + row * C::PH + colh) =
                             make_double2(hs[2 * h], hs[2 * h + 1]);
                 }
             } else {
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const int col = 4 * cq + e - R;  // Hx column (x - (x0 - R))
+                for (int e = 0; e < EPL; ++e) {
+                    const int col = EPL * cq + e - R;  // Hx column (x - (x0 - R))
                     if (valid && col >= 0 && col < C::E1X) Hx[row * C::PH + col] = hs[e];
                 }
             }
@@ -785,7 +860,7 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     };
     static_assert(C::K3 % 2 == 0, "P3 works on pairs");
     auto do_p3 = [&](int tid, int zc) {  // y-window (f64) of Hx -> U; a, b -> Lab
-        const int item = tid - C::T3;
+        const int item = p3_item(tid);
         if (item < 0) return;
         if constexpr (ABL & 2048) return;
         const int col = item % C::E1X, sg = item / C::E1X;
@@ -991,7 +1066,7 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     // Positions outside the domain either read 0 through the range check or read a neighbour
     // row's value that is never used (P3 zeroes its out-of-domain (a, b); P5's store drops).
     auto load_p3v = [&](rsrc_t r) {
-        const int item = (int)threadIdx.x - C::T3;
+        const int item = p3_item((int)threadIdx.x);
         const int col = item % C::E1X, sg = item / C::E1X;
         const int gx = x0 - R + col, gy0 = y0 - R + sg * C::K3;
 #pragma unroll
@@ -1009,7 +1084,7 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
         for (int j = 0; j < K5; ++j) {
             const int oy = oyb + j;
             const bool ok = ox < ox_end && oy < oy_end;
-            v5[j] = Buf<TIn>::load(r, opaque(ok ? (oy * sy + ox) * ESZ : kBadOff));
+            v5[j] = Buf<TIn>::template load<GF_V5_AUX>(r, opaque(ok ? (oy * sy + ox) * ESZ : kBadOff));
         }
     };
     float* const dummy = reinterpret_cast<float*>(smem + C::OFF_DUMMY);  // inactive lanes' writes
@@ -1041,6 +1116,7 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     load_p1(slice_rsrc(zc_begin + R), slice_rsrc(zc_begin - R - 1));
 #if GF_DIRECT
     load_p3v(slice_rsrc(zc_begin));
+    if constexpr (C::ONEBAR) set_hx(zc_begin);
     do_p12(tid0);
 #else
     load_c(slice_rsrc(zc_begin));
@@ -1060,7 +1136,7 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     const int64_t off_c = (int64_t)(R + 1) * sstride, off_a = (int64_t)(2 * R + 1) * sstride;
     int zb = zc_begin + 1 - R;
     int64_t ob = (int64_t)(zb - p.in_z0) * sstride;
-    int zs = zc_begin - 1 - R;
+    int zs = zc_begin - (C::ONEBAR ? 2 : 1) - R;  // output slice of this step's P5
     int64_t os = (int64_t)(zs - p.oz0) * osstride;
     const char* out_base = static_cast<const char*>(p.out);
     const unsigned nzo = (unsigned)(zo_end - zo_begin);
@@ -1072,13 +1148,44 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     // The step count is padded to a multiple of W, at least one past the last stage-1 slice so
     // that P5/the store of the last output slice happen inside the loop: no guards inside.
     // Padded steps emit nothing (zo >= zo_end).
-    const int n_steps = (zc_end - zc_begin + 1 + W - 1) / W * W;
+    // (ONEBAR: P5 runs two steps behind P3, so one more step.)
+    const int n_steps = (zc_end - zc_begin + (C::ONEBAR ? 2 : 1) + W - 1) / W * W;
     for (int i0 = zc_begin; i0 < zc_begin + n_steps; i0 += W) {
         static_for<0, W>([&](auto kc) {
             constexpr int k = decltype(kc)::value;
             const int i = i0 + k;
             const int tid = threadIdx.x;
             const rsrc_t r_b = rs_in(ob, zb);
+            if constexpr (C::ONEBAR) {
+                // One barrier per step. Step i: P12(i+1) -> Hx[i+1], P5(i-2) <- Hab[i],
+                // P3(i) <- Hx[i] -> Lab[i], P4(i-1) <- Lab[i-1] -> Hab[i-1] (buffers by parity:
+                // each is written in one step and read in the next). The first steps' P4/P5
+                // work on unwritten buffers for slices that lie in no emitted window (see the
+                // GF_DIRECT note on P5); their stores go to zero-record descriptors.
+                ro5 = make_rsrc(out_base + os,
+                                (unsigned)(zs - zo_begin) < nzo ? oslice_bytes : 0u);
+                if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(3);
+                set_hx(i + 1);
+                do_p12(tid);
+                load_p1(rs_in(ob + off_a, zb + 2 * R + 1), r_b);  // for P12(i+2)
+                if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(1);
+                set_hab(i);
+                do_p5(tid, i - 2, std::integral_constant<int, (k + 2 * W - 2) % W>{});
+                load_p5v(rs_in(ob - 2 * sstride, zb - 2));  // slice i-1-R, for P5(i-1)
+                set_hx(i);
+                set_lab(i);
+                do_p3(tid, i);
+                load_p3v(rs_in(ob + (int64_t)R * sstride, zb + R));  // slice i+1, for P3(i+1)
+                set_lab(i - 1);
+                set_hab(i - 1);
+                do_p4(tid);
+                lds_barrier_abl<ABL>();
+                ++zb;
+                ob += sstride;
+                ++zs;
+                os += osstride;
+                return;
+            }
             // tools/ instrumentation only (ABL & 16384): per-wave stamps of one workgroup
             auto stamp = [&](int slot) {
                 if constexpr (ABL & 16384) {
