@@ -192,6 +192,11 @@ int zt_synth_step_noise_f32(zt_ctx* ctx, float* out, const int64_t* shape, int n
 /* u16 = ((splitmix64(seed ^ global_index) >> 40) * 65535) >> 24. */
 int zt_synth_u16(zt_ctx* ctx, uint16_t* out, const int64_t* shape, int ndim,
                  const int64_t* global_shape, int64_t z0, uint64_t seed);
+/* The box [start, start + shape) of the N-d global synthetic volume (kind 0: float32 step+noise,
+ * kind 1: uint16 noise), element for element the values the whole-array generators give it: a
+ * rank generates its own octant / slab of a global array (benchmarks, parity samples). */
+int zt_synth_box(zt_ctx* ctx, int kind, void* out, const int64_t* start, const int64_t* shape,
+                 const int64_t* global_shape, int ndim, uint64_t seed);
 
 
 /* ---- Gaussian (src/filter/filters/gaussian.rs; src/filter/kernel.rs) ----------------------- */

@@ -85,3 +85,111 @@ def test_slab_assignment_covers_rows_once():
                 assert a.in_z0 == max(a.out_z0 - 8, 0)
                 assert a.in_z0 + a.in_nz == min(a.out_z0 + a.out_nz + 8, n_rows)
         assert (seen == 1).all()
+
+
+# ---- zarrs_ome pyramid: octant ownership (shard.octant_assignment) ---------------------------
+
+from zarrs_tools_amd.shard import assemble_chunk, octant_assignment, pyramid_level_shapes  # noqa: E402
+
+
+def _oracle_levels(v, factor, n):
+    out, cur = [], v
+    for _ in range(n):
+        cur = O.downsample(cur, "uint16", factor, "uint16")
+        out.append(cur)
+    return out
+
+
+def _octant_union(shape, factor, max_levels, world, gen):
+    """Every rank's locally computed levels (the oracle standing in for the device kernel),
+    assembled on the host level by level; levels past local_levels by rank 0 from the assembled
+    level local_levels. Returns the assembled pyramid."""
+    v = gen(shape)
+    per_rank = []
+    for r in range(world):
+        a = octant_assignment(r, world, shape, factor, max_levels)
+        if a.coord is None:
+            per_rank.append((a, []))
+            continue
+        box = v[tuple(slice(s, s + n) for s, n in zip(a.start, a.shape))]
+        per_rank.append((a, _oracle_levels(box, factor, a.local_levels)))
+    a0 = per_rank[0][0]
+    shapes = pyramid_level_shapes(shape, factor, max_levels)
+    assert a0.levels == len(shapes)
+    assembled = []
+    for k in range(a0.local_levels):
+        pieces = [(a.level_boxes[k][0], lv[k]) for a, lv in per_rank if a.coord is not None]
+        for a, lv in per_rank:
+            if a.coord is not None:
+                assert lv[k].shape == a.level_boxes[k][1]
+        assembled.append(assemble_chunk((0,) * len(shape), shapes[k], pieces))
+    if a0.levels > a0.local_levels:
+        assembled += _oracle_levels(assembled[-1], factor, a0.levels - a0.local_levels)
+    return v, assembled
+
+
+@pytest.mark.parametrize("shape,factor,world", [
+    ((64, 48, 80), (2, 2, 2), 8), ((64, 48, 80), (2, 2, 2), 2), ((50, 37, 70), (2, 2, 2), 2),
+    ((50, 37, 70), (2, 2, 2), 8), ((3, 8, 12), (2, 2, 2), 8), ((40, 36, 70), (2, 1, 2), 4),
+    ((96, 64), (2, 2), 3), ((17, 33, 65), (3, 2, 2), 6)])
+def test_octant_union_equals_global_pyramid(shape, factor, world):
+    v, got = _octant_union(shape, factor, 10, world, O.synth_u16)
+    want = _oracle_levels(v, factor, len(pyramid_level_shapes(shape, factor, 10)))
+    assert len(got) == len(want)
+    for g, w in zip(got, want):
+        np.testing.assert_array_equal(g, w)
+
+
+def test_octant_boxes_cover_each_level_once():
+    shape, factor = (4096, 4096, 4096), (2, 2, 2)
+    for world in (1, 2, 4, 8):
+        shapes = pyramid_level_shapes(shape, factor, 5)
+        for k in range(5):
+            vol = 0
+            for r in range(world):
+                a = octant_assignment(r, world, shape, factor, 5)
+                assert a.local_levels == 5 and a.coord is not None
+                vol += int(np.prod(a.level_boxes[k][1]))
+            assert vol == int(np.prod(shapes[k]))
+    # config P: every rank owns a 2048^3 octant, levels 1-5 local (1024^3 .. 64^3)
+    a = octant_assignment(7, 8, shape, factor, 5)
+    assert a.shape == (2048,) * 3 and a.level_boxes[-1] == ((64, 64, 64), (64, 64, 64))
+
+
+def _octant_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        shape, factor = (48, 40, 72), (2, 2, 2)
+        a = octant_assignment(rank, world, shape, factor, 10)
+        # this rank's box of the global synthetic volume, generated locally
+        box = O.synth_block_nd(a.start, a.shape, shape, "uint16")
+        mine = _oracle_levels(box, factor, a.local_levels)
+        got = [None] * world
+        dist.all_gather_object(got, (a.level_boxes, [m.tolist() for m in mine]))
+        if rank == 0:
+            shapes = pyramid_level_shapes(shape, factor, 10)
+            levels = []
+            for k in range(a.local_levels):
+                pieces = [(lb[k][0], np.array(lv[k], dtype=np.uint16)) for lb, lv in got]
+                levels.append(assemble_chunk((0, 0, 0), shapes[k], pieces))
+            q.put(levels)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_octant_split_gloo_world2_equals_whole_pyramid():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_octant_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    levels = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = _oracle_levels(O.synth_u16((48, 40, 72)), (2, 2, 2), len(levels))
+    for g, w in zip(levels, want):
+        np.testing.assert_array_equal(g, w)

@@ -23,13 +23,15 @@ from .filter import (  # noqa: E402
     pyramid_level_shapes,
     synth_step_noise_f32,
     synth_u16,
+    synth_box,
     torch_dtype,
 )
-from .shard import SlabAssignment, slab_assignment  # noqa: E402
+from .shard import OctantAssignment, SlabAssignment, octant_assignment, slab_assignment  # noqa: E402
 
 __all__ = [
     "ArraySubset", "ArraySubsetOverlap", "Context", "DeviceArray", "Downsample", "DTYPES",
     "FilterError", "Gaussian", "GuidedFilter", "InvalidParameters", "SlabAssignment", "UnsupportedDataType",
-    "default_context", "dtype_of", "lib", "pyramid", "pyramid_level_shapes", "slab_assignment",
-    "synth_step_noise_f32", "synth_u16", "torch_dtype",
+    "default_context", "dtype_of", "lib", "octant_assignment", "OctantAssignment", "pyramid",
+    "pyramid_level_shapes", "slab_assignment",
+    "synth_step_noise_f32", "synth_u16", "synth_box", "torch_dtype",
 ]

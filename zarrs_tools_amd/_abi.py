@@ -153,6 +153,7 @@ def lib() -> ctypes.CDLL:
         "zt_synth_step_noise_f32": ([vp, vp, i64p, c_int, i64p, ctypes.c_int64, ctypes.c_uint64],
                                     c_int),
         "zt_synth_u16": ([vp, vp, i64p, c_int, i64p, ctypes.c_int64, ctypes.c_uint64], c_int),
+        "zt_synth_box": ([vp, c_int, vp, i64p, i64p, i64p, c_int, ctypes.c_uint64], c_int),
         # store -> store path (host storage)
         "zt_store_array_info": ([ctypes.c_char_p, ctypes.POINTER(c_int), ctypes.POINTER(c_int),
                                  i64p, i64p, i64p], c_int),

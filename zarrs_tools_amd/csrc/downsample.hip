@@ -179,6 +179,53 @@ __global__ void synth_u16_kernel(uint16_t* __restrict__ out, int64_t n, int64_t 
     }
 }
 
+// The box [start, start + shape) of an N-d global synthetic volume (kind 0: step+noise f32,
+// kind 1: u16 noise): element values of the global linear index, as the whole-array generators.
+struct SynthBox {
+    int ndim;
+    int64_t start[kMaxDims], shape[kMaxDims], gshape[kMaxDims];
+};
+
+__global__ void synth_box_kernel(void* __restrict__ out, int kind, int64_t n, SynthBox b,
+                                 uint64_t seed) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        int64_t rem = i, gl = 0, mul = 1, gx = 0;
+        for (int d = b.ndim - 1; d >= 0; --d) {
+            const int64_t c = rem % b.shape[d] + b.start[d];
+            rem /= b.shape[d];
+            gl += c * mul;
+            mul *= b.gshape[d];
+            if (d == b.ndim - 1) gx = c;
+        }
+        const uint64_t h = splitmix64(seed ^ (uint64_t)gl);
+        if (kind == 0) {
+            const float U = (float)(h >> 40) * (1.0f / 16777216.0f);
+            const float t = __fmul_rn(100.0f, U);
+            static_cast<float*>(out)[i] =
+                __fadd_rn(t, gx >= b.gshape[b.ndim - 1] / 2 ? 500.0f : 0.0f);
+        } else {
+            static_cast<uint16_t*>(out)[i] = (uint16_t)(((h >> 40) * 65535ull) >> 24);
+        }
+    }
+}
+
+hipError_t launch_synth_box(void* out, int kind, const int64_t* start, const int64_t* shape,
+                            const int64_t* gshape, int ndim, uint64_t seed, hipStream_t s) {
+    SynthBox b{};
+    b.ndim = ndim;
+    int64_t n = 1;
+    for (int d = 0; d < ndim; ++d) {
+        b.start[d] = start[d];
+        b.shape[d] = shape[d];
+        b.gshape[d] = gshape[d];
+        n *= shape[d];
+    }
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(synth_box_kernel, dim3(256 * 64), dim3(256), 0, s, out, kind, n, b, seed);
+    return hipGetLastError();
+}
+
 hipError_t launch_synth_step_noise_f32(float* out, int64_t n, int64_t plane, int64_t nx_row,
                                        int64_t nx_global, int64_t z0, uint64_t seed,
                                        hipStream_t s) {

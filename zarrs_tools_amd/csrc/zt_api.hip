@@ -956,4 +956,22 @@ int zt_synth_u16(zt_ctx* ctx, uint16_t* out, const int64_t* shape, int ndim,
     return ZT_OK;
 }
 
+int zt_synth_box(zt_ctx* ctx, int kind, void* out, const int64_t* start, const int64_t* shape,
+                 const int64_t* global_shape, int ndim, uint64_t seed) {
+    if (int rc = check_ctx(ctx)) return rc;
+    if (int rc = check_shape(shape, ndim, "shape")) return rc;
+    if (int rc = check_shape(global_shape, ndim, "global_shape")) return rc;
+    if (!start) return fail(ZT_ERR_INVALID_PARAMETERS, "null start");
+    if (kind != 0 && kind != 1) return fail(ZT_ERR_INVALID_PARAMETERS, "kind must be 0 or 1");
+    for (int d = 0; d < ndim; ++d)
+        if (start[d] < 0 || start[d] + shape[d] > global_shape[d])
+            return fail(ZT_ERR_INVALID_PARAMETERS, "box outside the global shape on axis %d", d);
+    if (numel(shape, ndim) == 0) return ZT_OK;
+    if (!out) return fail(ZT_ERR_INVALID_PARAMETERS, "null data pointer");
+    DeviceGuard g(ctx->device);
+    hipError_t e = zt::launch_synth_box(out, kind, start, shape, global_shape, ndim, seed, ctx->cur);
+    if (e != hipSuccess) return hip_fail(e, "synth launch");
+    return ZT_OK;
+}
+
 }  // extern "C"

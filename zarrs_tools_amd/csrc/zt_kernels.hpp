@@ -103,5 +103,7 @@ hipError_t launch_synth_step_noise_f32(float* out, int64_t n, int64_t plane, int
                                        hipStream_t s);
 hipError_t launch_synth_u16(uint16_t* out, int64_t n, int64_t plane, int64_t z0, uint64_t seed,
                             hipStream_t s);
+hipError_t launch_synth_box(void* out, int kind, const int64_t* start, const int64_t* shape,
+                            const int64_t* gshape, int ndim, uint64_t seed, hipStream_t s);
 
 }  // namespace zt

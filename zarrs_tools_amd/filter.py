@@ -464,3 +464,17 @@ def synth_u16(shape, seed: int = 0x5EED2025, global_shape=None, z0: int = 0, dev
     check(lib().zt_synth_u16(ctx.handle, _ptr(out), i64_array(shape), len(shape), i64_array(gs),
                              int(z0), int(seed)))
     return out
+
+
+def synth_box(start, shape, global_shape, kind: str = "uint16", seed: int = 0x5EED2025,
+              device=None, ctx: Optional[Context] = None):
+    """The box [start, start+shape) of the global synthetic volume, generated on the device
+    (kind "uint16" noise or "float32" step+noise): a rank's own octant or slab."""
+    torch = _torch()
+    dt = torch.uint16 if kind == "uint16" else torch.float32
+    out = torch.empty(tuple(shape), dtype=dt, device=device or "cuda")
+    ctx = ctx or default_context(out.device.index)
+    check(lib().zt_synth_box(ctx.handle, 1 if kind == "uint16" else 0, _ptr(out),
+                             i64_array(start), i64_array(shape), i64_array(global_shape),
+                             len(shape), int(seed)))
+    return out

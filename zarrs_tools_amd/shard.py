@@ -67,16 +67,20 @@ def pyramid_level_shapes(shape, factor, max_levels: int) -> list:
 class OctantAssignment:
     rank: int
     world: int
-    grid: tuple          # ranks per axis
-    coord: tuple         # this rank's position in the rank grid
-    start: tuple         # level-0 box start (multiple of factor^L per axis)
-    shape: tuple         # level-0 box shape
-    level_boxes: tuple   # ((start, shape) of the owned box of level k) for k = 1..L
+    grid: tuple          # ranks per axis (their product may be < world: the rest own nothing)
+    coord: tuple         # this rank's position in the rank grid (None: owns nothing)
+    start: tuple         # level-0 box start (multiple of factor^local_levels per axis)
+    shape: tuple         # level-0 box shape (zeros: owns nothing)
+    local_levels: int    # levels every rank computes on its own box (1..L)
+    level_boxes: tuple   # ((start, shape) of the owned box of level k) for k = 1..local_levels
+    levels: int          # all levels of the pyramid; levels past local_levels are computed by
+                         # rank 0 from the assembled level local_levels (small by construction)
 
 
 def _rank_grid(world: int, units) -> tuple:
-    """Factor `world` over the axes, each prime factor to the axis with the most aligned units
-    per rank (ties: the slowest axis), never splitting an axis below one unit per rank."""
+    """Factor `world` over the axes, each prime factor (largest first) to the axis with the
+    most aligned units per rank, never below one unit per rank (ties: the slowest axis).
+    Factors that fit no axis are dropped: the product may be less than `world`."""
     grid = [1] * len(units)
     n, p, primes = world, 2, []
     while n > 1:
@@ -85,23 +89,42 @@ def _rank_grid(world: int, units) -> tuple:
             n //= p
         p += 1
     for p in sorted(primes, reverse=True):
-        best = max(range(len(units)), key=lambda d: (units[d] // (grid[d] * p) >= 1,
-                                                      units[d] / grid[d], -d))
-        if units[best] // (grid[best] * p) < 1:
-            raise ValueError(f"cannot split {list(units)} aligned units over {world} ranks")
+        fits = [d for d in range(len(units)) if units[d] // (grid[d] * p) >= 1]
+        if not fits:
+            continue
+        best = max(fits, key=lambda d: (units[d] / grid[d], -d))
         grid[best] *= p
     return tuple(grid)
 
 
 def octant_assignment(rank: int, world: int, shape, factor, max_levels: int) -> OctantAssignment:
-    """The level-0 box rank `rank` of `world` owns and its box at every pyramid level."""
+    """The level-0 box rank `rank` of `world` owns and its box at every locally computed level:
+    the most levels L whose factor^L-aligned split still uses all ranks (else the split using
+    the most ranks)."""
     if world < 1 or not 0 <= rank < world:
         raise ValueError("bad rank/world")
     levels = pyramid_level_shapes(shape, factor, max_levels)
-    L = len(levels)
+    nd = len(shape)
+    best = None
+    for L in range(len(levels), 0, -1):
+        units = [s // (f ** L) for s, f in zip(shape, factor)]
+        g = _rank_grid(world, units)
+        n = 1
+        for x in g:
+            n *= x
+        if best is None or n > best[0]:
+            best = (n, L, g)
+        if n == world:
+            break
+    if best is None:  # no levels at all
+        return OctantAssignment(rank, world, (1,) * nd, None if rank else (0,) * nd,
+                                (0,) * nd, tuple(shape) if rank == 0 else (0,) * nd, 0, (), 0)
+    nranks, L, grid = best
+    if rank >= nranks:
+        return OctantAssignment(rank, world, grid, None, (0,) * nd, (0,) * nd, L, (),
+                                len(levels))
     align = [f ** L for f in factor]
     units = [s // a for s, a in zip(shape, align)]
-    grid = _rank_grid(world, units)
     coord, r = [], rank
     for g in reversed(grid):
         coord.append(r % g)
@@ -117,10 +140,11 @@ def octant_assignment(rank: int, world: int, shape, factor, max_levels: int) -> 
         fk = [f ** k for f in factor]
         s_k = [a // f for a, f in zip(start, fk)]
         e_k = [levels[k - 1][d] if coord[d] == grid[d] - 1 else end[d] // fk[d]
-               for d in range(len(shape))]
+               for d in range(nd)]
         boxes.append((tuple(s_k), tuple(b - a for a, b in zip(s_k, e_k))))
     return OctantAssignment(rank, world, grid, coord, tuple(start),
-                            tuple(b - a for a, b in zip(start, end)), tuple(boxes))
+                            tuple(b - a for a, b in zip(start, end)), L, tuple(boxes),
+                            len(levels))
 
 
 def assemble_chunk(chunk_start, chunk_shape, pieces):
