@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define ZT_ABI_VERSION 1
+#define ZT_ABI_VERSION 2
 #define ZT_MAX_DIMS 8
 
 /* Status codes. Negative values mirror FilterError variants (src/filter/filter_error.rs:10-30). */
@@ -244,7 +244,21 @@ typedef struct zt_store_stats {
     uint64_t voxels;                   /* output elements produced */
     int64_t rows;                      /* output chunk rows processed */
     int threads;                       /* host worker threads used */
+    int rows_in_flight;                /* input chunk rows held decoded (memory-bounded) */
+    int double_buffered;               /* 1: device slabs / output rows double buffered */
 } zt_store_stats;
+
+/* Per-chunk progress of the store filters (Progress / ProgressCallback, progress.rs:15-119):
+ * after every output chunk is written, `fn` receives the step count, the number of steps (output
+ * chunks of the call) and the cumulative read (decode thread-seconds), process (device seconds)
+ * and write (encode thread-seconds) durations. Called from the host worker threads, serialised;
+ * process-wide; NULL disables. */
+typedef struct zt_progress {
+    int64_t step, num_steps;
+    double read_s, process_s, write_s;
+} zt_progress;
+typedef void (*zt_progress_fn)(const zt_progress* progress, void* user);
+void zt_store_set_progress_callback(zt_progress_fn fn, void* user);
 
 /* flags for the store filters */
 #define ZT_STORE_ERASE_OUTPUT_METADATA 1 /* remove OUT/zarr.json first ("not finished" marker,
@@ -262,7 +276,8 @@ int zt_store_create_array(const char* path, int dtype, int ndim, const int64_t* 
                           const char* fill_value_json);
 /* The output array the filters create: the input's shape, chunking and codecs with data type
  * dtype_out (-1 = the input's) and the input fill value cast to it (filter_traits.rs:47-82). */
-int zt_store_create_output_like(const char* in_path, const char* out_path, int dtype_out);
+int zt_store_create_output_like(const char* in_path, const char* out_path, int dtype_out,
+                                const char* encoding_json);
 /* Read any subset into a C-order host buffer (missing chunks read as the fill value). */
 int zt_store_read_subset(const char* path, const int64_t* start, const int64_t* shape,
                          void* host_out, int nthreads);
@@ -273,22 +288,34 @@ int zt_store_write_subset(const char* path, const int64_t* start, const int64_t*
  * kind 1: uint16 noise), identical to zt_synth_step_noise_f32 / zt_synth_u16. */
 int zt_store_write_synth(const char* path, int kind, uint64_t seed, int nthreads);
 
+/* encoding_json (NULL or "" = the input's encoding): a JSON object with the reencoding
+ * arguments of the filter commands (ZarrReencodingArgs, lib.rs:274-377; applied as
+ * get_array_builder_reencode, lib.rs:408-650): "data_type", "fill_value", "separator",
+ * "chunk_shape", "shard_shape", "array_to_array_codecs" (only []), "array_to_bytes_codec" (bytes),
+ * "bytes_to_bytes_codecs" (gzip / zstd / crc32c), "dimension_names", "attributes",
+ * "attributes_append". A "data_type" there takes precedence over dtype_out. Output arrays whose
+ * chunk rows do not fit 80 % of the available host / device memory (with no overlap) fail with
+ * ZT_ERR_OUT_OF_MEMORY, as calculate_chunk_limit does (filter.rs:52-66). */
 /* zarrs_filter guided-filter IN OUT EPS R [--data-type T] over a store (GuidedFilter::apply,
  * guided_filter.rs:240-319): the output array is IN's shape/chunking/codecs with dtype_out (-1 =
  * input type). Processes the output chunk rows [row_begin, row_end) along axis 0 (row_end < 0 =
  * all), so ranks can split the rows; the array's zarr.json is written only with
  * ZT_STORE_FINISH_OUTPUT. nthreads <= 0: min(16, hardware threads). stats may be NULL. */
 int zt_store_guided_filter(const char* in_path, const char* out_path, int dtype_out,
-                           float epsilon, int radius, int device, int64_t row_begin,
-                           int64_t row_end, int nthreads, int flags, zt_store_stats* stats);
+                           const char* encoding_json, float epsilon, int radius, int device,
+                           int64_t row_begin, int64_t row_end, int nthreads, int flags,
+                           zt_store_stats* stats);
 /* zarrs_filter downsample / one zarrs_ome level over a store (Downsample::apply,
- * downsample.rs:170-286; output chunk = min(input chunk, output shape), zarrs_ome.rs:549-559). */
+ * downsample.rs:170-286): output shape max(n / stride, 1), encoding as the input's with the
+ * encoding_json overrides (zarrs_ome passes its per-level chunk / shard shapes). */
 int zt_store_downsample(const char* in_path, const char* out_path, const int64_t* stride,
-                        int discrete, int dtype_out, int device, int64_t row_begin,
-                        int64_t row_end, int nthreads, int flags, zt_store_stats* stats);
+                        int discrete, int dtype_out, const char* encoding_json, int device,
+                        int64_t row_begin, int64_t row_end, int nthreads, int flags,
+                        zt_store_stats* stats);
 /* zarrs_filter gaussian IN OUT SIGMA HALF [--data-type T] over a store (Gaussian::apply,
  * gaussian.rs:170-249): as zt_store_guided_filter, halo = kernel_half_size. */
-int zt_store_gaussian(const char* in_path, const char* out_path, int dtype_out, const float* sigma,
+int zt_store_gaussian(const char* in_path, const char* out_path, int dtype_out,
+                      const char* encoding_json, const float* sigma,
                       const int64_t* kernel_half_size, int device, int64_t row_begin,
                       int64_t row_end, int nthreads, int flags, zt_store_stats* stats);
 /* One zarrs_ome level with --gaussian-sigma (apply_chunk_continuous_gaussian, zarrs_ome.rs:
@@ -296,8 +323,9 @@ int zt_store_gaussian(const char* in_path, const char* out_path, int dtype_out, 
  * the mean downsample of that f32 block to the level's data type. */
 int zt_store_downsample_gaussian(const char* in_path, const char* out_path, const int64_t* stride,
                                  const float* sigma, const int64_t* kernel_half_size,
-                                 int dtype_out, int device, int64_t row_begin, int64_t row_end,
-                                 int nthreads, int flags, zt_store_stats* stats);
+                                 int dtype_out, const char* encoding_json, int device,
+                                 int64_t row_begin, int64_t row_end, int nthreads, int flags,
+                                 zt_store_stats* stats);
 /* 1 if the named codec can be read and written here, else 0. */
 int zt_store_codec_available(const char* name);
 

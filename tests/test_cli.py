@@ -101,3 +101,53 @@ def test_exists_erase_removes_stale_chunks_under_tmp(tmp_path, monkeypatch):
         ZF.run([{"filter": "guided_filter", "input": str(tmp_path / "in"), "output": str(out),
                  "epsilon": 1.0, "radius": 1}], tmp=str(tmp_path), log=lambda *a: None)
     assert calls and not (out / "c" / "stale").exists()
+
+
+def test_reencoding_args_on_every_filter():
+    # ZarrReencodingArgs flattened into the filter arguments (filter_common_arguments.rs:7-16)
+    a = ZF.build_parser().parse_args([
+        "guided-filter", "i", "o", "1", "2", "-d", "float32", "-f", "NaN", "-s", "256,256,256",
+        "-c", "32,32,32", "--bytes-to-bytes-codecs", '[{"name": "gzip", "configuration": {"level": 5}}]',
+        "--separator", ".", "--dimension-names", "z,y,x", "--attributes", '{"k": 1}'])
+    st = ZF._steps_from_cli(a)[0]
+    enc = ZF.encoding_of(st)
+    assert enc == {"data_type": "float32", "fill_value": "NaN", "separator": ".",
+                   "chunk_shape": [32, 32, 32], "shard_shape": [256, 256, 256],
+                   "bytes_to_bytes_codecs": [{"name": "gzip", "configuration": {"level": 5}}],
+                   "dimension_names": ["z", "y", "x"], "attributes": {"k": 1}}
+    for sub in (["downsample", "i", "o", "2,2"], ["gaussian", "i", "o", "1,1", "3,3"]):
+        a = ZF.build_parser().parse_args(sub + ["--shard-shape", "0,64", "--fill-value", "3"])
+        assert ZF.encoding_of(ZF._steps_from_cli(a)[0]) == {"shard_shape": [0, 64],
+                                                           "fill_value": 3}
+    # run-config form: JSON strings or values
+    assert ZF.encoding_of({"filter": "downsample", "chunk_shape": "8,8",
+                           "attributes_append": '{"a": 2}'}) == {
+        "chunk_shape": [8, 8], "attributes_append": {"a": 2}}
+    assert ZF.encoding_of({"filter": "downsample"}) is None
+
+
+def test_ome_cli_surface_and_helpers():
+    a = ZO.build_parser().parse_args(["i", "o", "2,2,1", "--physical-size", "0.5,0.5,1",
+                                      "--physical-units", "micrometer,second,channel",
+                                      "--group-attributes", '{"g": 1}', "--exists", "overwrite",
+                                      "-s", "64,64,64", "-c", "32,32,32"])
+    assert a.factor == [2, 2, 1] and a.physical_size == [0.5, 0.5, 1.0]
+    assert a.exists == "overwrite" and a.shard_shape == [64, 64, 64]
+    # units_to_axis (zarrs_ome.rs:390-432)
+    assert ZO.axis_of("z", "micrometer") == {"name": "z", "type": "space", "unit": "micrometer"}
+    assert ZO.axis_of("t", "second") == {"name": "t", "type": "time", "unit": "second"}
+    assert ZO.axis_of("c", "channel") == {"name": "c", "type": "channel"}
+    assert ZO.axis_of("q", "furlong") == {"name": "q", "unit": "furlong"}
+    assert ZO.axis_of("0", None) == {"name": "0"}
+
+
+def test_ome_level_encoding_rule(tmp_path):
+    # zarrs_ome.rs:528-560
+    S.create_array(tmp_path / "a", "uint16", (40, 36, 70), (16, 16, 32))
+    assert ZO.level_encoding(S.open_array(tmp_path / "a"), (20, 18, 35)) == {
+        "chunk_shape": [16, 16, 32]}
+    assert ZO.level_encoding(S.open_array(tmp_path / "a"), (5, 4, 8)) == {"chunk_shape": [5, 4, 8]}
+    S.create_array(tmp_path / "b", "uint16", (40, 36, 70), (32, 32, 32),
+                   S.codecs_json(None, shard_inner=(8, 16, 16)))
+    assert ZO.level_encoding(S.open_array(tmp_path / "b"), (20, 18, 35)) == {
+        "shard_shape": [20, 18, 32], "chunk_shape": [8, 16, 16]}

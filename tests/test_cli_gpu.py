@@ -90,3 +90,79 @@ def test_zarrs_ome_extent3_factor2_scale(tmp_path):
     ct = meta["attributes"]["ome"]["multiscales"][0]["datasets"][1]["coordinateTransformations"]
     assert ct[0]["scale"] == [3.0, 2.0, 2.0]
     assert ct[1]["translation"] == [1.0, 0.5, 0.5]
+
+
+def test_guided_filter_with_reencoding_args(tmp_path):
+    # -d float32 -s 32,32,32 -c 16,16,16 --bytes-to-bytes-codecs gzip: a sharded gzip output
+    shape, chunk = (40, 44, 48), (16, 16, 16)
+    u = O.synth_u16(shape)
+    S.create_array(tmp_path / "in.zarr", "uint16", shape, chunk)
+    S.write_array(tmp_path / "in.zarr", u)
+    rc = ZF.main(["guided-filter", str(tmp_path / "in.zarr"), str(tmp_path / "out.zarr"),
+                  "40000", "2", "-d", "float32", "-s", "32,32,32", "-c", "16,16,16",
+                  "--bytes-to-bytes-codecs", '[{"name": "gzip", "configuration": {"level": 1}}]',
+                  "--dimension-names", "z,y,x"])
+    assert rc == 0
+    m = json.load(open(tmp_path / "out.zarr" / "zarr.json"))
+    assert m["data_type"] == "float32" and m["dimension_names"] == ["z", "y", "x"]
+    assert m["chunk_grid"]["configuration"]["chunk_shape"] == [32, 32, 32]
+    assert m["codecs"][0]["name"] == "sharding_indexed"
+    ref = O.guided_filter_apply(u.astype(np.float32), chunk, 40000.0, 2, nthreads=8)
+    assert rel_err(S.read_array(tmp_path / "out.zarr"), ref) <= FLOAT_TOL
+
+
+def test_zarrs_ome_sharded_levels_reencoded_level0_and_axes(tmp_path):
+    shape = (40, 36, 70)
+    u = O.synth_u16(shape)
+    S.create_array(tmp_path / "in.zarr", "uint16", shape, (16, 16, 32))
+    S.write_array(tmp_path / "in.zarr", u)
+    rc = ZO.main([str(tmp_path / "in.zarr"), str(tmp_path / "ome"), "--max-levels", "3",
+                  "-s", "32,32,64", "-c", "16,16,32", "--physical-units",
+                  "micrometer,micrometer,micrometer", "--physical-size", "2,1,1",
+                  "--group-attributes", '{"note": "x"}', "--name", "vol"])
+    assert rc == 0
+    m0 = json.load(open(tmp_path / "ome" / "0" / "zarr.json"))
+    assert m0["codecs"][0]["name"] == "sharding_indexed"  # level 0 reencoded (zarrs_ome.rs:355)
+    np.testing.assert_array_equal(S.read_array(tmp_path / "ome" / "0"), u)
+    want = u
+    for lv in (1, 2, 3):
+        want = O.downsample(want, "uint16", (2, 2, 2), "uint16")
+        np.testing.assert_array_equal(S.read_array(tmp_path / "ome" / str(lv)), want)
+        m = json.load(open(tmp_path / "ome" / str(lv) / "zarr.json"))
+        assert m["codecs"][0]["name"] == "sharding_indexed"
+    g = json.load(open(tmp_path / "ome" / "zarr.json"))["attributes"]
+    assert g["note"] == "x"
+    ms = g["ome"]["multiscales"][0]
+    assert ms["name"] == "vol" and ms["type"] == "average"
+    assert ms["axes"][0] == {"name": "0", "type": "space", "unit": "micrometer"}
+    assert ms["coordinateTransformations"] == [{"type": "scale", "scale": [2.0, 1.0, 1.0]}]
+
+
+def test_store_progress_callback_counts_output_chunks(tmp_path):
+    shape, chunk = (40, 44, 48), (16, 16, 16)
+    S.create_array(tmp_path / "in.zarr", "float32", shape, chunk)
+    S.write_synth(tmp_path / "in.zarr")
+    seen = []
+    S.set_progress_callback(seen.append)
+    try:
+        S.guided_filter(tmp_path / "in.zarr", tmp_path / "out.zarr", 2500.0, 2)
+    finally:
+        S.set_progress_callback(None)
+    n = 3 * 3 * 3
+    assert [p["step"] for p in seen] == list(range(1, n + 1))
+    assert all(p["num_steps"] == n for p in seen)
+    assert seen[-1]["read_s"] > 0 and seen[-1]["write_s"] > 0 and seen[-1]["process_s"] > 0
+
+
+def test_store_single_buffered_under_a_small_memory_budget(tmp_path, monkeypatch):
+    # calculate_chunk_limit analogue: too little host memory for overlap -> one row in flight,
+    # same result
+    shape, chunk = (64, 48, 64), (16, 48, 64)
+    S.create_array(tmp_path / "in.zarr", "float32", shape, chunk)
+    S.write_synth(tmp_path / "in.zarr")
+    row = 16 * 48 * 64 * 4
+    monkeypatch.setenv("ZT_STORE_HOST_MEMORY", str(int(4 * row / 0.8) + 1024))
+    st = S.guided_filter(tmp_path / "in.zarr", tmp_path / "out.zarr", 2500.0, 2)
+    assert st["double_buffered"] == 0 and st["rows_in_flight"] == 3
+    ref = O.guided_filter_apply(O.synth_step_noise_f32(shape), chunk, 2500.0, 2, nthreads=8)
+    assert rel_err(S.read_array(tmp_path / "out.zarr"), ref) <= FLOAT_TOL

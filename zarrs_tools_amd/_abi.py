@@ -69,13 +69,24 @@ STORE_ERASE_OUTPUT_METADATA = 1
 STORE_FINISH_OUTPUT = 2
 
 
+class Progress(ctypes.Structure):
+    """zt_progress (include/zarrs_tools_amd.h): Progress stats of progress.rs:6-13."""
+    _fields_ = [("step", ctypes.c_int64), ("num_steps", ctypes.c_int64),
+                ("read_s", ctypes.c_double), ("process_s", ctypes.c_double),
+                ("write_s", ctypes.c_double)]
+
+
+PROGRESS_FN = ctypes.CFUNCTYPE(None, ctypes.POINTER(Progress), ctypes.c_void_p)
+
+
 class StoreStats(ctypes.Structure):
     """zt_store_stats (include/zarrs_tools_amd.h)."""
     _fields_ = [("wall_s", ctypes.c_double), ("decode_s", ctypes.c_double),
                 ("encode_s", ctypes.c_double), ("h2d_s", ctypes.c_double),
                 ("kernel_s", ctypes.c_double), ("d2h_s", ctypes.c_double),
                 ("bytes_read", ctypes.c_uint64), ("bytes_written", ctypes.c_uint64),
-                ("voxels", ctypes.c_uint64), ("rows", ctypes.c_int64), ("threads", ctypes.c_int)]
+                ("voxels", ctypes.c_uint64), ("rows", ctypes.c_int64), ("threads", ctypes.c_int),
+                ("rows_in_flight", ctypes.c_int), ("double_buffered", ctypes.c_int)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -159,22 +170,24 @@ def lib() -> ctypes.CDLL:
                                  i64p, i64p, i64p], c_int),
         "zt_store_create_array": ([ctypes.c_char_p, c_int, c_int, i64p, i64p, ctypes.c_char_p,
                                    ctypes.c_char_p], c_int),
-        "zt_store_create_output_like": ([ctypes.c_char_p, ctypes.c_char_p, c_int], c_int),
+        "zt_store_create_output_like": ([ctypes.c_char_p, ctypes.c_char_p, c_int,
+                                         ctypes.c_char_p], c_int),
+        "zt_store_set_progress_callback": ([PROGRESS_FN, vp], None),
         "zt_store_read_subset": ([ctypes.c_char_p, i64p, i64p, vp, c_int], c_int),
         "zt_store_write_subset": ([ctypes.c_char_p, i64p, i64p, vp, c_int], c_int),
         "zt_store_write_synth": ([ctypes.c_char_p, c_int, ctypes.c_uint64, c_int], c_int),
-        "zt_store_guided_filter": ([ctypes.c_char_p, ctypes.c_char_p, c_int, c_float, c_int,
-                                    c_int, ctypes.c_int64, ctypes.c_int64, c_int, c_int,
-                                    ctypes.POINTER(StoreStats)], c_int),
-        "zt_store_downsample": ([ctypes.c_char_p, ctypes.c_char_p, i64p, c_int, c_int, c_int,
-                                 ctypes.c_int64, ctypes.c_int64, c_int, c_int,
-                                 ctypes.POINTER(StoreStats)], c_int),
-        "zt_store_gaussian": ([ctypes.c_char_p, ctypes.c_char_p, c_int, fp, i64p, c_int,
-                               ctypes.c_int64, ctypes.c_int64, c_int, c_int,
+        "zt_store_guided_filter": ([ctypes.c_char_p, ctypes.c_char_p, c_int, ctypes.c_char_p,
+                                    c_float, c_int, c_int, ctypes.c_int64, ctypes.c_int64, c_int,
+                                    c_int, ctypes.POINTER(StoreStats)], c_int),
+        "zt_store_downsample": ([ctypes.c_char_p, ctypes.c_char_p, i64p, c_int, c_int,
+                                 ctypes.c_char_p, c_int, ctypes.c_int64, ctypes.c_int64, c_int,
+                                 c_int, ctypes.POINTER(StoreStats)], c_int),
+        "zt_store_gaussian": ([ctypes.c_char_p, ctypes.c_char_p, c_int, ctypes.c_char_p, fp, i64p,
+                               c_int, ctypes.c_int64, ctypes.c_int64, c_int, c_int,
                                ctypes.POINTER(StoreStats)], c_int),
         "zt_store_downsample_gaussian": ([ctypes.c_char_p, ctypes.c_char_p, i64p, fp, i64p, c_int,
-                                          c_int, ctypes.c_int64, ctypes.c_int64, c_int, c_int,
-                                          ctypes.POINTER(StoreStats)], c_int),
+                                          ctypes.c_char_p, c_int, ctypes.c_int64, ctypes.c_int64,
+                                          c_int, c_int, ctypes.POINTER(StoreStats)], c_int),
         "zt_store_codec_available": ([ctypes.c_char_p], c_int),
     }
     for name, (args, res) in sig.items():

@@ -254,28 +254,207 @@ uint64_t splitmix64(uint64_t x) {
     return x ^ (x >> 31);
 }
 
-// Convert a fill value to another data type with Rust `as` semantics (lib.rs convert_fill_value).
+// Convert a fill value to another data type with Rust `as` semantics (convert_fill_value,
+// lib.rs:836-899, num_traits::AsPrimitive): float -> int saturates (NaN -> 0) and truncates
+// toward zero, int -> int wraps, anything -> float rounds to nearest.
 zt::json::Value convert_fill(const Array& a, int dtype_out) {
     const uint8_t* f = a.fill.data();
+    bool is_float = false, is_signed = false;
     double v = 0.0;
+    int64_t iv = 0;
+    uint64_t uv = 0;
     switch (a.dtype) {
-    case ZT_BOOL: case ZT_UINT8: v = f[0]; break;
-    case ZT_INT8: v = (int8_t)f[0]; break;
-    case ZT_INT16: { int16_t x; std::memcpy(&x, f, 2); v = x; break; }
-    case ZT_INT32: { int32_t x; std::memcpy(&x, f, 4); v = x; break; }
-    case ZT_INT64: { int64_t x; std::memcpy(&x, f, 8); v = (double)x; break; }
-    case ZT_UINT16: { uint16_t x; std::memcpy(&x, f, 2); v = x; break; }
-    case ZT_UINT32: { uint32_t x; std::memcpy(&x, f, 4); v = x; break; }
-    case ZT_UINT64: { uint64_t x; std::memcpy(&x, f, 8); v = (double)x; break; }
-    case ZT_BFLOAT16: { uint16_t x; std::memcpy(&x, f, 2); v = zt::bf16_bits_to_f32(x); break; }
-    case ZT_FLOAT16: { uint16_t x; std::memcpy(&x, f, 2); v = zt::f16_bits_to_f32(x); break; }
-    case ZT_FLOAT32: { float x; std::memcpy(&x, f, 4); v = x; break; }
-    case ZT_FLOAT64: std::memcpy(&v, f, 8); break;
+    case ZT_BOOL: case ZT_UINT8: uv = f[0]; break;
+    case ZT_INT8: iv = (int8_t)f[0]; is_signed = true; break;
+    case ZT_INT16: { int16_t x; std::memcpy(&x, f, 2); iv = x; is_signed = true; break; }
+    case ZT_INT32: { int32_t x; std::memcpy(&x, f, 4); iv = x; is_signed = true; break; }
+    case ZT_INT64: { int64_t x; std::memcpy(&x, f, 8); iv = x; is_signed = true; break; }
+    case ZT_UINT16: { uint16_t x; std::memcpy(&x, f, 2); uv = x; break; }
+    case ZT_UINT32: { uint32_t x; std::memcpy(&x, f, 4); uv = x; break; }
+    case ZT_UINT64: { std::memcpy(&uv, f, 8); break; }
+    case ZT_BFLOAT16: { uint16_t x; std::memcpy(&x, f, 2); v = zt::bf16_bits_to_f32(x); is_float = true; break; }
+    case ZT_FLOAT16: { uint16_t x; std::memcpy(&x, f, 2); v = zt::f16_bits_to_f32(x); is_float = true; break; }
+    case ZT_FLOAT32: { float x; std::memcpy(&x, f, 4); v = x; is_float = true; break; }
+    case ZT_FLOAT64: std::memcpy(&v, f, 8); is_float = true; break;
     }
-    if (dtype_out < ZT_BFLOAT16 && dtype_out != ZT_BOOL) {
-        if (std::isnan(v)) v = 0.0;  // `as` maps NaN to 0 for integers
+    if (!is_float) {
+        if (is_signed) uv = (uint64_t)iv;
+        v = is_signed ? (double)iv : (double)uv;
     }
-    return zt::zarr::fill_json_from_double(dtype_out, v);
+    if (dtype_out >= ZT_BFLOAT16) return zt::zarr::fill_json_from_double(dtype_out, v);
+    // integer (and bool, as u8) targets
+    int bits = 8;
+    bool sgn = false;
+    switch (dtype_out) {
+    case ZT_INT8: sgn = true; bits = 8; break;
+    case ZT_INT16: sgn = true; bits = 16; break;
+    case ZT_INT32: sgn = true; bits = 32; break;
+    case ZT_INT64: sgn = true; bits = 64; break;
+    case ZT_UINT16: bits = 16; break;
+    case ZT_UINT32: bits = 32; break;
+    case ZT_UINT64: bits = 64; break;
+    default: bits = 8; break;  // bool, uint8
+    }
+    uint64_t out;
+    if (is_float) {  // saturating
+        if (std::isnan(v)) out = 0;
+        else if (sgn) {
+            const double lo = -std::ldexp(1.0, bits - 1), hi = std::ldexp(1.0, bits - 1);
+            const double t = std::trunc(v);
+            out = t <= lo ? (uint64_t)(int64_t)lo : t >= hi ? (uint64_t)((int64_t)(hi - 1 >= 9.2e18 ? INT64_MAX : (int64_t)hi - 1))
+                                                         : (uint64_t)(int64_t)t;
+        } else {
+            const double hi = std::ldexp(1.0, bits);
+            const double t = std::trunc(v);
+            out = t <= 0 ? 0 : t >= hi ? (bits == 64 ? UINT64_MAX : (uint64_t)hi - 1) : (uint64_t)t;
+        }
+    } else {
+        out = uv;  // wrapping
+    }
+    if (bits < 64) out &= ((uint64_t)1 << bits) - 1;
+    if (dtype_out == ZT_BOOL) return zt::json::Value(out != 0);
+    if (sgn) {
+        int64_t sv = (int64_t)(out << (64 - bits)) >> (64 - bits);  // sign-extend
+        return zt::json::Value(sv);
+    }
+    return zt::json::Value((uint64_t)out);
+}
+
+// ---- the output array of a filter: FilterTraits::output_array_builder (filter_traits.rs:47-82)
+//      + get_array_builder_reencode (lib.rs:408-650) ---------------------------------------------
+//
+// `enc` is a JSON object with ZarrReencodingArgs' keys (lib.rs:274-377): data_type, fill_value,
+// separator, chunk_shape, shard_shape, array_to_array_codecs, array_to_bytes_codec,
+// bytes_to_bytes_codecs, dimension_names, attributes, attributes_append; absent keys keep the
+// input's. Restated as the reference computes it, quirks included:
+//  * the base is the input array (shape, chunk grid, key encoding, attributes, dimension names);
+//  * an unsharded input's base "chunk shape" is its chunk GRID shape (lib.rs:447), and a chunk
+//    shape (override or base) only takes effect when the output is sharded: without a shard
+//    shape the output keeps the input's chunk grid (lib.rs:623-646);
+//  * shard = min(shard, input extent) (0 = the input extent), rounded up to a multiple of the
+//    chunk shape; chunk 0 = the input extent (lib.rs:462-494);
+//  * a new data type without a fill value converts the input fill value (`as` semantics).
+// Codecs supported here: bytes, gzip, zstd, crc32c, sharding_indexed (no array -> array codecs).
+Array build_output(const Array& in, const std::string& out_path, int dtype_filter,
+                   const std::vector<int64_t>& out_shape, const char* enc_json) {
+    using zt::json::Value;
+    Value enc = (enc_json && *enc_json) ? zt::json::parse(enc_json) : Value(zt::json::Object{});
+    if (!enc.is_obj())
+        throw zt::zarr::Error(ZT_ERR_INVALID_PARAMETERS, "encoding: a JSON object expected");
+    static const char* known[] = {"data_type", "fill_value", "separator", "chunk_shape",
+                                  "shard_shape", "array_to_array_codecs", "array_to_bytes_codec",
+                                  "bytes_to_bytes_codecs", "dimension_names", "attributes",
+                                  "attributes_append"};
+    for (const auto& kv : *enc.o) {
+        bool ok = false;
+        for (const char* k : known) ok = ok || kv.first == k;
+        if (!ok) throw zt::zarr::Error(ZT_ERR_INVALID_PARAMETERS, "encoding: unknown key " + kv.first);
+    }
+    const int nd = in.ndim();
+    auto ints = [&](const Value& v, const char* what) {
+        std::vector<int64_t> r;
+        if (!v.is_arr() || (int)v.arr().size() != nd)
+            throw zt::zarr::Error(ZT_ERR_INVALID_PARAMETERS,
+                                  std::string("encoding: ") + what + " needs one entry per axis");
+        for (const auto& x : v.arr()) r.push_back(x.as_int());
+        return r;
+    };
+    // base: the input's chunk / shard shapes and codec chain (lib.rs:414-458)
+    std::vector<int64_t> chunk, shard;
+    bool sharded = false;
+    zt::zarr::CodecChain chain;  // the (inner) chain: bytes + b2b
+    if (in.codecs.sharded) {
+        chunk = in.codecs.inner_shape;
+        shard = in.chunk_shape;
+        sharded = true;
+        chain = *in.codecs.inner;
+    } else {
+        chunk = in.grid_shape();
+        chain = in.codecs;
+    }
+    if (const Value* c = enc.find("chunk_shape")) {
+        chunk = ints(*c, "chunk_shape");
+        for (int d = 0; d < nd; ++d) if (chunk[d] == 0) chunk[d] = in.shape[d];
+    }
+    if (const Value* sv = enc.find("shard_shape")) {
+        shard = ints(*sv, "shard_shape");
+        for (int d = 0; d < nd; ++d) shard[d] = shard[d] == 0 ? in.shape[d] : std::min(shard[d], in.shape[d]);
+        sharded = true;
+    }
+    if (sharded)
+        for (int d = 0; d < nd; ++d) {
+            if (chunk[d] <= 0) throw zt::zarr::Error(ZT_ERR_INVALID_PARAMETERS, "encoding: chunk extents must be positive");
+            shard[d] = (shard[d] + chunk[d] - 1) / chunk[d] * chunk[d];  // next_multiple_of
+        }
+    if (const Value* a2a = enc.find("array_to_array_codecs")) {
+        const Value v = a2a->is_str() ? zt::json::parse(a2a->str()) : *a2a;
+        if (!v.is_arr() || !v.arr().empty())
+            throw zt::zarr::Error(ZT_ERR_INVALID_PARAMETERS,
+                                  "encoding: array to array codecs are not supported on this path");
+    }
+    // the chain JSON [array_to_bytes, bytes_to_bytes...], overrides applied
+    Value inner_js = chain.to_json();
+    Value a2b = inner_js.arr().at(0);
+    std::vector<Value> b2b(inner_js.arr().begin() + 1, inner_js.arr().end());
+    if (const Value* v = enc.find("array_to_bytes_codec")) a2b = v->is_str() ? zt::json::parse(v->str()) : *v;
+    if (const Value* v = enc.find("bytes_to_bytes_codecs")) {
+        const Value l = v->is_str() ? zt::json::parse(v->str()) : *v;
+        if (!l.is_arr()) throw zt::zarr::Error(ZT_ERR_INVALID_PARAMETERS, "encoding: bytes_to_bytes_codecs must be a list");
+        b2b = l.arr();
+    }
+    zt::json::Array inner_list{a2b};
+    for (auto& c : b2b) inner_list.push_back(c);
+    Value codecs;
+    std::vector<int64_t> grid_chunk;
+    if (sharded) {
+        Value cfg = Value(zt::json::Object{});
+        cfg.set("chunk_shape", Value([&] { zt::json::Array a; for (auto c : chunk) a.push_back(Value(c)); return a; }()));
+        cfg.set("codecs", Value(inner_list));
+        cfg.set("index_codecs", zt::json::parse(
+            "[{\"name\":\"bytes\",\"configuration\":{\"endian\":\"little\"}},{\"name\":\"crc32c\"}]"));
+        cfg.set("index_location", "end");
+        Value sh = Value(zt::json::Object{});
+        sh.set("name", "sharding_indexed");
+        sh.set("configuration", cfg);
+        codecs = Value(zt::json::Array{sh});
+        grid_chunk = shard;
+    } else {
+        codecs = Value(inner_list);
+        grid_chunk = in.chunk_shape;  // the builder keeps the input's chunk grid
+    }
+    // data type and fill value (filter_traits.rs:53-74, lib.rs:585-611)
+    int dt = in.dtype;
+    bool dt_changed = false;
+    if (const Value* v = enc.find("data_type")) {
+        dt = zt::zarr::dtype_from_name(v->str());
+        if (dt < 0) throw zt::zarr::Error(ZT_ERR_UNSUPPORTED_DATA_TYPE, "unsupported data type " + v->str());
+        dt_changed = true;
+    } else if (dtype_filter >= 0 && dtype_filter != in.dtype) {
+        dt = dtype_filter;
+        dt_changed = true;
+    }
+    Value fill = in.fill_json;
+    if (const Value* v = enc.find("fill_value")) fill = *v;
+    else if (dt_changed) fill = convert_fill(in, dt);
+    Array out = Array::create(out_path, dt, out_shape, grid_chunk, codecs, fill);
+    out.key_encoding = in.key_encoding;
+    out.separator = in.separator;
+    if (const Value* v = enc.find("separator")) {
+        const std::string sep = v->str();
+        if (sep != "/" && sep != ".")
+            throw zt::zarr::Error(ZT_ERR_INVALID_PARAMETERS, "encoding: separator must be / or .");
+        out.key_encoding = "default";  // chunk_key_encoding_default_separator (lib.rs:585-587)
+        out.separator = sep[0];
+    }
+    out.attributes = in.attributes.is_null() ? Value(zt::json::Object{}) : in.attributes;
+    if (const Value* v = enc.find("attributes")) out.attributes = v->is_str() ? zt::json::parse(v->str()) : *v;
+    if (const Value* v = enc.find("attributes_append")) {
+        const Value add = v->is_str() ? zt::json::parse(v->str()) : *v;
+        if (add.is_obj()) for (const auto& kv : *add.o) out.attributes.set(kv.first, kv.second);
+    }
+    out.dimension_names = in.dimension_names;
+    if (const Value* v = enc.find("dimension_names")) out.dimension_names = *v;
+    return out;
 }
 
 int report(const std::exception& e) {
@@ -286,7 +465,48 @@ int report(const std::exception& e) {
 // ---- the chunk-row pipeline --------------------------------------------------------------------
 
 // What one output chunk row needs from the input and how it is computed on the device.
+// ---- calculate_chunk_limit (filter.rs:52-66) for the row pipeline ------------------------------
+// The reference bounds the chunks in flight by 80 % of the available RAM / memory_per_chunk and
+// fails with FilterError::Other when not even one chunk fits. Here the unit in flight is a chunk
+// row (pinned host rows, device slabs): the ring depth and double buffering are chosen from 80 %
+// of the available host RAM and 80 % of the free device memory, down to one row without overlap,
+// and the reference's error is returned when not even that fits. ZT_STORE_HOST_MEMORY /
+// ZT_STORE_DEVICE_MEMORY (bytes) override the available amounts (tests, co-tenant limits).
+uint64_t host_available_bytes() {
+    if (const char* e = std::getenv("ZT_STORE_HOST_MEMORY")) return std::strtoull(e, nullptr, 10);
+    FILE* f = std::fopen("/proc/meminfo", "r");
+    uint64_t kb = 0;
+    if (f) {
+        char line[256];
+        while (std::fgets(line, sizeof line, f))
+            if (std::sscanf(line, "MemAvailable: %lu kB", (unsigned long*)&kb) == 1) break;
+        std::fclose(f);
+    }
+    return kb ? kb * 1024 : (uint64_t)16 << 30;
+}
+
+uint64_t device_available_bytes() {
+    if (const char* e = std::getenv("ZT_STORE_DEVICE_MEMORY")) return std::strtoull(e, nullptr, 10);
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return fr;
+}
+
+const char* kNotEnoughMemory =
+    "There is not enough available memory to process a single output chunk. Consider reducing "
+    "the chunk shape (or shard shape if sharding)";
+
+// ---- progress (Progress / ProgressCallback, progress.rs:15-119) ---------------------------------
+std::mutex g_progress_mu;
+zt_progress_fn g_progress_fn = nullptr;
+void* g_progress_user = nullptr;
+
 struct RowOp {
+    // device scratch the transform allocates for a slab of `planes` input planes (estimate)
+    std::function<uint64_t(int64_t planes)> scratch_bytes;
     // input planes along axis 0 for output planes [z0, z1)
     std::function<void(int64_t z0, int64_t z1, int64_t& in0, int64_t& in1)> input_planes;
     // run the transform: slab (input planes [in0, in1)) -> out (output planes [z0, z1))
@@ -324,10 +544,28 @@ void run_pipeline(const Array& in, const Array& out, int device, int64_t row_beg
         max_slab = std::max(max_slab, b - a);
         max_rows_per = std::max(max_rows_per, j1 - j0 + 1);
     }
-    const int64_t NR = max_rows_per + 2;  // ring of decoded input rows (+1 decoding ahead, +1 slack)
+    // memory budget: ring depth NR (rows decoded ahead) and NB (double-buffered slabs / outputs)
+    const uint64_t in_row_b = (uint64_t)in_cz * in_pb, out_row_b = (uint64_t)out_cz * out_pb;
+    const uint64_t host_budget = host_available_bytes() / 10 * 8;
+    int64_t NR = max_rows_per + 2;  // ring of decoded input rows (+1 decoding ahead, +1 slack)
+    int NB = 2;
+    while (NR * in_row_b + (uint64_t)NB * out_row_b > host_budget) {
+        if (NR > max_rows_per) --NR;
+        else if (NB > 1) NB = 1;
+        else throw zt::zarr::Error(ZT_ERR_OUT_OF_MEMORY, kNotEnoughMemory);
+    }
 
     if (hipSetDevice(device) != hipSuccess)
         throw zt::zarr::Error(ZT_ERR_DEVICE, "hipSetDevice failed");
+    {
+        const uint64_t scratch = op.scratch_bytes ? op.scratch_bytes(max_slab) : 0;
+        const uint64_t dev_budget = device_available_bytes() / 10 * 8;
+        auto dev_need = [&](int nb) {
+            return (uint64_t)nb * ((uint64_t)max_slab * in_pb + out_row_b) + scratch;
+        };
+        if (dev_need(NB) > dev_budget) NB = 1;
+        if (dev_need(NB) > dev_budget) throw zt::zarr::Error(ZT_ERR_OUT_OF_MEMORY, kNotEnoughMemory);
+    }
     Ctx ctx;
     if (int rc = zt_ctx_create(device, &ctx.c)) throw zt::zarr::Error(rc, zt_last_error());
     Streams streams;
@@ -346,9 +584,9 @@ void run_pipeline(const Array& in, const Array& out, int device, int64_t row_beg
     std::vector<Pinned> hin(NR);
     for (auto& h : hin) h.alloc((size_t)in_cz * in_pb);
     Pinned hout[2];
-    for (auto& h : hout) h.alloc((size_t)out_cz * out_pb);
+    for (int s = 0; s < NB; ++s) hout[s].alloc((size_t)out_cz * out_pb);
     DevBuf dslab[2], dout[2];
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < NB; ++s) {
         dslab[s].alloc((size_t)max_slab * in_pb);
         dout[s].alloc((size_t)out_cz * out_pb);
     }
@@ -358,8 +596,10 @@ void run_pipeline(const Array& in, const Array& out, int device, int64_t row_beg
     Group enc_group[2];
     std::vector<int64_t> ring_row(NR, -1);
     std::atomic<uint64_t> bytes_read{0}, bytes_written{0};
-    std::atomic<int64_t> dec_ns{0}, enc_ns{0};
+    std::atomic<int64_t> dec_ns{0}, enc_ns{0}, k_us{0}, chunks_done{0};
     double h2d_ms = 0, k_ms = 0, d2h_ms = 0;
+    int64_t chunks_total = 0;
+    for (int64_t k = row_begin; k < row_end; ++k) chunks_total += (int64_t)chunks_in_rows(out, k, k + 1).size();
 
     // region descriptors of a host row buffer (C order, in_cz planes)
     std::vector<int64_t> in_row_shape(in.shape);
@@ -390,7 +630,7 @@ void run_pipeline(const Array& in, const Array& out, int device, int64_t row_beg
         }
     };
     auto submit_encode = [&](int64_t k) {
-        const int s = (int)(k % 2);
+        const int s = (int)(k % NB);
         uint8_t* buf = hout[s].u8();
         for (auto& idx : chunks_in_rows(out, k, k + 1)) {
             pool.submit(enc_group[s], [&, idx, buf, k] {
@@ -401,6 +641,17 @@ void run_pipeline(const Array& in, const Array& out, int device, int64_t row_beg
                                            out_row_st.data());
                 bytes_written += n;
                 enc_ns += (int64_t)(secs_since(t0) * 1e9);
+                const int64_t step = ++chunks_done;  // Progress::next (progress.rs:101-104)
+                std::lock_guard<std::mutex> lk(g_progress_mu);
+                if (g_progress_fn) {
+                    zt_progress pr{};
+                    pr.step = step;
+                    pr.num_steps = chunks_total;
+                    pr.read_s = dec_ns.load() * 1e-9;
+                    pr.process_s = k_us.load() * 1e-6;
+                    pr.write_s = enc_ns.load() * 1e-9;
+                    g_progress_fn(&pr, g_progress_user);
+                }
             });
         }
     };
@@ -414,10 +665,12 @@ void run_pipeline(const Array& in, const Array& out, int device, int64_t row_beg
     const int64_t in_rows_total = (nz_in + in_cz - 1) / in_cz;
     int64_t pending_enc = -1;  // output row whose D2H is queued but not yet handed to the encoders
     auto finish_row = [&](int64_t k) {
-        const int s = (int)(k % 2);
+        const int s = (int)(k % NB);
         HIPCHK(hipEventSynchronize(ev_d2h[s]));
         h2d_ms += ev_ms(ev_h2d0[s], ev_h2d[s]);
-        k_ms += ev_ms(ev_k0[s], ev_k[s]);
+        const float km = ev_ms(ev_k0[s], ev_k[s]);
+        k_ms += km;
+        k_us += (int64_t)(km * 1e3f);
         d2h_ms += ev_ms(ev_d2h0[s], ev_d2h[s]);
         submit_encode(k);
     };
@@ -433,10 +686,14 @@ void run_pipeline(const Array& in, const Array& out, int device, int64_t row_beg
             const int64_t want = std::min(std::max(j1, nj1), in_rows_total - 1);
             while (next_dec <= want && next_dec - NR < j0) submit_decode(next_dec++);
             for (int64_t j = j0; j <= j1; ++j) dec_group[j % NR].wait();
-            const int s = (int)(k % 2);
-            enc_group[s].wait();  // host output buffer s is free again (row k-2 encoded)
+            const int s = (int)(k % NB);
+            if (NB == 1 && pending_enc >= 0) {  // single buffer: row k-1 is encoded first
+                finish_row(pending_enc);
+                pending_enc = -1;
+            }
+            enc_group[s].wait();  // host output buffer s is free again (row k-NB encoded)
             // H2D: the slab's planes from the ring rows that hold them
-            HIPCHK(hipStreamWaitEvent(s_h2d, ev_k[s], 0));  // kernel k-2 no longer reads slab s
+            HIPCHK(hipStreamWaitEvent(s_h2d, ev_k[s], 0));  // kernel k-NB no longer reads slab s
             HIPCHK(hipEventRecord(ev_h2d0[s], s_h2d));
             for (int64_t j = j0; j <= j1; ++j) {
                 const int64_t p0 = std::max(in0, j * in_cz), p1 = std::min(in1, (j + 1) * in_cz);
@@ -451,7 +708,7 @@ void run_pipeline(const Array& in, const Array& out, int device, int64_t row_beg
             }
             // kernel
             HIPCHK(hipStreamWaitEvent(s_comp, ev_h2d[s], 0));
-            HIPCHK(hipStreamWaitEvent(s_comp, ev_d2h[s], 0));  // D2H k-2 done with dout[s]
+            HIPCHK(hipStreamWaitEvent(s_comp, ev_d2h[s], 0));  // D2H k-NB done with dout[s]
             HIPCHK(hipEventRecord(ev_k0[s], s_comp));
             const int64_t z0 = k * out_cz, z1 = std::min(z0 + out_cz, nz_out);
             if (int rc = op.apply(ctx.c, dslab[s].p, in0, in1, dout[s].p, z0, z1))
@@ -492,6 +749,8 @@ void run_pipeline(const Array& in, const Array& out, int device, int64_t row_beg
         st->voxels = (uint64_t)vox;
         st->rows = row_end - row_begin;
         st->threads = pool.size();
+        st->rows_in_flight = (int)NR;
+        st->double_buffered = NB == 2;
     }
 }
 
@@ -679,13 +938,12 @@ int zt_store_write_synth(const char* path, int kind, uint64_t seed, int nthreads
     }
 }
 
-int zt_store_create_output_like(const char* in_path, const char* out_path, int dtype_out) {
+int zt_store_create_output_like(const char* in_path, const char* out_path, int dtype_out,
+                                const char* encoding_json) {
     try {
         if (!in_path || !out_path) return zt::set_last_error(ZT_ERR_INVALID_PARAMETERS, "null path");
         Array in = Array::open(in_path);
-        const int dt = dtype_out < 0 ? in.dtype : dtype_out;
-        Array out = Array::create(out_path, dt, in.shape, in.chunk_shape, in.codecs.to_json(),
-                                  dt == in.dtype ? in.fill_json : convert_fill(in, dt));
+        Array out = build_output(in, out_path, dtype_out, in.shape, encoding_json);
         out.store_metadata();
         return ZT_OK;
     } catch (const std::exception& e) {
@@ -694,19 +952,19 @@ int zt_store_create_output_like(const char* in_path, const char* out_path, int d
 }
 
 int zt_store_guided_filter(const char* in_path, const char* out_path, int dtype_out,
-                           float epsilon, int radius, int device, int64_t row_begin,
-                           int64_t row_end, int nthreads, int flags, zt_store_stats* stats) {
+                           const char* encoding_json, float epsilon, int radius, int device,
+                           int64_t row_begin, int64_t row_end, int nthreads, int flags,
+                           zt_store_stats* stats) {
     try {
         if (!in_path || !out_path) return zt::set_last_error(ZT_ERR_INVALID_PARAMETERS, "null path");
         if (radius < 0 || radius > 127)
             return zt::set_last_error(ZT_ERR_INVALID_PARAMETERS, "radius must be in [0, 127]");
         Array in = Array::open(in_path);
-        const int dt = dtype_out < 0 ? in.dtype : dtype_out;
+        // output_array_builder: the input's shape, with the reencoding overrides and data type
+        // (filter_traits.rs:47-82, lib.rs:408-650)
+        Array out = build_output(in, out_path, dtype_out, in.shape, encoding_json);
+        const int dt = out.dtype;
         if (int rc = zt_guided_filter_is_compatible(in.dtype, dt)) return rc;
-        // output_array_builder: same shape, chunking and codecs; data type (and converted fill
-        // value) from --data-type (filter_traits.rs:47-82, lib.rs:409-650)
-        Array out = Array::create(out_path, dt, in.shape, in.chunk_shape, in.codecs.to_json(),
-                                  dt == in.dtype ? in.fill_json : convert_fill(in, dt));
         if (flags & ZT_STORE_ERASE_OUTPUT_METADATA) out.erase_metadata();  // "not finished" marker
         const int nd = in.ndim();
         const int64_t halo = (int64_t)((radius * 2) & 0xFF);  // u8 arithmetic (guided_filter.rs:92)
@@ -718,6 +976,13 @@ int zt_store_guided_filter(const char* in_path, const char* out_path, int dtype_
         };
         const std::vector<int64_t> shape = in.shape, chunk = in.chunk_shape;
         const int din = in.dtype;
+        int64_t plane = 1;
+        for (int d = 1; d < nd; ++d) plane *= shape[d];
+        op.scratch_bytes = [&](int64_t planes) -> uint64_t {
+            // separable path (n-D or r > 8): 5 f32 words per slab voxel; fused path: f32 staging
+            // of non-direct element types
+            return (uint64_t)planes * plane * ((nd == 3 && radius <= 8) ? 8 : 20);
+        };
         op.apply = [&](zt_ctx* c, const void* slab, int64_t in0, int64_t in1, void* o, int64_t z0,
                        int64_t z1) -> int {
             if (nd == 3 && radius <= 8)
@@ -743,34 +1008,23 @@ int zt_store_guided_filter(const char* in_path, const char* out_path, int dtype_
 }
 
 int zt_store_downsample(const char* in_path, const char* out_path, const int64_t* stride,
-                        int discrete, int dtype_out, int device, int64_t row_begin,
-                        int64_t row_end, int nthreads, int flags, zt_store_stats* stats) {
+                        int discrete, int dtype_out, const char* encoding_json, int device,
+                        int64_t row_begin, int64_t row_end, int nthreads, int flags,
+                        zt_store_stats* stats) {
     try {
         if (!in_path || !out_path || !stride)
             return zt::set_last_error(ZT_ERR_INVALID_PARAMETERS, "null argument");
         Array in = Array::open(in_path);
         const int nd = in.ndim();
-        const int dt = dtype_out < 0 ? in.dtype : dtype_out;
-        if (int rc = zt_downsample_is_compatible(in.dtype, dt, discrete)) return rc;
         std::vector<int64_t> st(stride, stride + nd), oshape(nd), win(nd);
         if (int rc = zt_downsample_output_shape(in.shape.data(), nd, st.data(), oshape.data()))
             return rc;
         for (int d = 0; d < nd; ++d) win[d] = std::min(st[d], in.shape[d]);
-        // zarrs_ome.rs:549-559: output chunk = min(input chunk, output shape) per axis
-        std::vector<int64_t> ochunk(nd);
-        for (int d = 0; d < nd; ++d) ochunk[d] = std::min(in.chunk_shape[d], oshape[d]);
-        zt::json::Value codecs = in.codecs.to_json();
-        if (in.codecs.sharded) {
-            // keep the inner chunk no larger than the (possibly shrunk) shard
-            Array probe = in;
-            for (int d = 0; d < nd; ++d)
-                probe.codecs.inner_shape[d] = std::min(in.codecs.inner_shape[d], ochunk[d]);
-            for (int d = 0; d < nd; ++d)
-                if (ochunk[d] % probe.codecs.inner_shape[d]) probe.codecs.inner_shape[d] = ochunk[d];
-            codecs = probe.codecs.to_json();
-        }
-        Array out = Array::create(out_path, dt, oshape, ochunk, codecs,
-                                  dt == in.dtype ? in.fill_json : convert_fill(in, dt));
+        // Downsample::output_array_builder: the output shape with the reencoding overrides
+        // (zarrs_ome passes its per-level chunk / shard shapes here, zarrs_ome.rs:528-560)
+        Array out = build_output(in, out_path, dtype_out, oshape, encoding_json);
+        const int dt = out.dtype;
+        if (int rc = zt_downsample_is_compatible(in.dtype, dt, discrete)) return rc;
         if (flags & ZT_STORE_ERASE_OUTPUT_METADATA) out.erase_metadata();
         const int din = in.dtype;
         const int64_t w0 = win[0];
@@ -795,7 +1049,8 @@ int zt_store_downsample(const char* in_path, const char* out_path, const int64_t
     }
 }
 
-int zt_store_gaussian(const char* in_path, const char* out_path, int dtype_out, const float* sigma,
+int zt_store_gaussian(const char* in_path, const char* out_path, int dtype_out,
+                      const char* encoding_json, const float* sigma,
                       const int64_t* kernel_half_size, int device, int64_t row_begin,
                       int64_t row_end, int nthreads, int flags, zt_store_stats* stats) {
     try {
@@ -803,13 +1058,12 @@ int zt_store_gaussian(const char* in_path, const char* out_path, int dtype_out, 
             return zt::set_last_error(ZT_ERR_INVALID_PARAMETERS, "null argument");
         Array in = Array::open(in_path);
         const int nd = in.ndim();
-        const int dt = dtype_out < 0 ? in.dtype : dtype_out;
-        if (int rc = zt_gaussian_is_compatible(in.dtype, dt)) return rc;
         for (int d = 0; d < nd; ++d)
             if (kernel_half_size[d] < 0)
                 return zt::set_last_error(ZT_ERR_INVALID_PARAMETERS, "negative kernel_half_size");
-        Array out = Array::create(out_path, dt, in.shape, in.chunk_shape, in.codecs.to_json(),
-                                  dt == in.dtype ? in.fill_json : convert_fill(in, dt));
+        Array out = build_output(in, out_path, dtype_out, in.shape, encoding_json);
+        const int dt = out.dtype;
+        if (int rc = zt_gaussian_is_compatible(in.dtype, dt)) return rc;
         if (flags & ZT_STORE_ERASE_OUTPUT_METADATA) out.erase_metadata();
         const int64_t halo = kernel_half_size[0], nz = in.shape[0];
         RowOp op;
@@ -821,6 +1075,11 @@ int zt_store_gaussian(const char* in_path, const char* out_path, int dtype_out, 
         const std::vector<float> sg(sigma, sigma + nd);
         const std::vector<int64_t> hs(kernel_half_size, kernel_half_size + nd);
         const int din = in.dtype;
+        int64_t gplane = 1;
+        for (int d = 1; d < nd; ++d) gplane *= shape[d];
+        op.scratch_bytes = [&](int64_t planes) -> uint64_t {
+            return (uint64_t)planes * gplane * 8;  // two f32 pass buffers
+        };
         op.apply = [&](zt_ctx* c, const void* slab, int64_t in0, int64_t in1, void* o, int64_t z0,
                        int64_t z1) -> int {
             // the slab is a block that carries the halo or reaches the array edge on axis 0 and
@@ -842,36 +1101,24 @@ int zt_store_gaussian(const char* in_path, const char* out_path, int dtype_out, 
 
 int zt_store_downsample_gaussian(const char* in_path, const char* out_path, const int64_t* stride,
                                  const float* sigma, const int64_t* kernel_half_size,
-                                 int dtype_out, int device, int64_t row_begin, int64_t row_end,
-                                 int nthreads, int flags, zt_store_stats* stats) {
+                                 int dtype_out, const char* encoding_json, int device,
+                                 int64_t row_begin, int64_t row_end, int nthreads, int flags,
+                                 zt_store_stats* stats) {
     try {
         if (!in_path || !out_path || !stride || !sigma || !kernel_half_size)
             return zt::set_last_error(ZT_ERR_INVALID_PARAMETERS, "null argument");
         Array in = Array::open(in_path);
         const int nd = in.ndim();
-        const int dt = dtype_out < 0 ? in.dtype : dtype_out;
-        if (int rc = zt_downsample_is_compatible(zt::kF32, dt, 0)) return rc;
         for (int d = 0; d < nd; ++d)
             if (kernel_half_size[d] < 0)
                 return zt::set_last_error(ZT_ERR_INVALID_PARAMETERS, "negative kernel_half_size");
-        std::vector<int64_t> st(stride, stride + nd), oshape(nd), win(nd), ochunk(nd);
+        std::vector<int64_t> st(stride, stride + nd), oshape(nd), win(nd);
         if (int rc = zt_downsample_output_shape(in.shape.data(), nd, st.data(), oshape.data()))
             return rc;
-        for (int d = 0; d < nd; ++d) {
-            win[d] = std::min(st[d], in.shape[d]);
-            ochunk[d] = std::min(in.chunk_shape[d], oshape[d]);  // zarrs_ome.rs:549-559
-        }
-        zt::json::Value codecs = in.codecs.to_json();
-        if (in.codecs.sharded) {
-            Array probe = in;
-            for (int d = 0; d < nd; ++d)
-                probe.codecs.inner_shape[d] = std::min(in.codecs.inner_shape[d], ochunk[d]);
-            for (int d = 0; d < nd; ++d)
-                if (ochunk[d] % probe.codecs.inner_shape[d]) probe.codecs.inner_shape[d] = ochunk[d];
-            codecs = probe.codecs.to_json();
-        }
-        Array out = Array::create(out_path, dt, oshape, ochunk, codecs,
-                                  dt == in.dtype ? in.fill_json : convert_fill(in, dt));
+        for (int d = 0; d < nd; ++d) win[d] = std::min(st[d], in.shape[d]);
+        Array out = build_output(in, out_path, dtype_out, oshape, encoding_json);
+        const int dt = out.dtype;
+        if (int rc = zt_downsample_is_compatible(zt::kF32, dt, 0)) return rc;
         if (flags & ZT_STORE_ERASE_OUTPUT_METADATA) out.erase_metadata();
         const int64_t w0 = win[0], halo = kernel_half_size[0], nz = in.shape[0];
         auto ds_planes = [&](int64_t z0, int64_t z1, int64_t& a, int64_t& b) {
@@ -913,6 +1160,12 @@ int zt_store_downsample_gaussian(const char* in_path, const char* out_path, cons
     } catch (const std::exception& e) {
         return report(e);
     }
+}
+
+void zt_store_set_progress_callback(zt_progress_fn fn, void* user) {
+    std::lock_guard<std::mutex> lk(g_progress_mu);
+    g_progress_fn = fn;
+    g_progress_user = user;
 }
 
 int zt_store_codec_available(const char* name) {

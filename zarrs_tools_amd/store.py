@@ -134,6 +134,45 @@ def codec_available(name: str) -> bool:
     return bool(lib().zt_store_codec_available(name.encode()))
 
 
+def _enc(encoding) -> Optional[bytes]:
+    """Reencoding arguments (ZarrReencodingArgs keys, lib.rs:274-377) as the ABI's JSON."""
+    if encoding is None:
+        return None
+    if isinstance(encoding, (bytes, str)):
+        return encoding.encode() if isinstance(encoding, str) else encoding
+    return json.dumps({k: v for k, v in encoding.items() if v is not None}).encode()
+
+
+_progress_keep = None
+
+
+def set_progress_callback(fn) -> None:
+    """Per-chunk progress of the store filters (Progress, progress.rs:15-119): `fn(stats)` with
+    stats = {step, num_steps, read_s, process_s, write_s} after every output chunk is written.
+    Process-wide; None disables."""
+    global _progress_keep
+    if fn is None:
+        lib().zt_store_set_progress_callback(_abi.PROGRESS_FN(), None)
+        _progress_keep = None
+        return
+
+    def _cb(p, _user):
+        s = p.contents
+        fn({"step": s.step, "num_steps": s.num_steps, "read_s": s.read_s,
+            "process_s": s.process_s, "write_s": s.write_s})
+
+    _progress_keep = _abi.PROGRESS_FN(_cb)
+    lib().zt_store_set_progress_callback(_progress_keep, None)
+
+
+def create_output_like(input_path, output_path, data_type: Optional[str] = None,
+                       encoding=None) -> None:
+    """The output array a filter creates (output_array_builder, filter_traits.rs:47-82), with
+    its zarr.json written."""
+    check(lib().zt_store_create_output_like(_b(input_path), _b(output_path), _dt(data_type),
+                                            _enc(encoding)))
+
+
 def _flags(erase: bool, finish: bool) -> int:
     return (_abi.STORE_ERASE_OUTPUT_METADATA if erase else 0) | (
         _abi.STORE_FINISH_OUTPUT if finish else 0)
@@ -141,25 +180,27 @@ def _flags(erase: bool, finish: bool) -> int:
 
 def guided_filter(input_path, output_path, epsilon: float, radius: int,
                   data_type: Optional[str] = None, device: int = 0, rows=None,
-                  nthreads: int = 0, erase: bool = True, finish: bool = True) -> dict:
+                  nthreads: int = 0, erase: bool = True, finish: bool = True,
+                  encoding=None) -> dict:
     """zarrs_filter guided-filter INPUT OUTPUT EPSILON RADIUS [--data-type T] on GPU `device`.
     `rows` = (begin, end) output chunk rows along axis 0 (None = all). Returns the run stats."""
     st = _abi.StoreStats()
     r0, r1 = (0, -1) if rows is None else (int(rows[0]), int(rows[1]))
     check(lib().zt_store_guided_filter(_b(input_path), _b(output_path), _dt(data_type),
-                                       float(epsilon), int(radius), int(device), r0, r1,
+                                       _enc(encoding), float(epsilon), int(radius), int(device), r0, r1,
                                        int(nthreads), _flags(erase, finish), ctypes.byref(st)))
     return st.as_dict()
 
 
 def downsample(input_path, output_path, stride, discrete: bool = False,
                data_type: Optional[str] = None, device: int = 0, rows=None, nthreads: int = 0,
-               erase: bool = True, finish: bool = True) -> dict:
+               erase: bool = True, finish: bool = True, encoding=None) -> dict:
     """zarrs_filter downsample INPUT OUTPUT STRIDE [--discrete] / one zarrs_ome level."""
     st = _abi.StoreStats()
     r0, r1 = (0, -1) if rows is None else (int(rows[0]), int(rows[1]))
     check(lib().zt_store_downsample(_b(input_path), _b(output_path), i64_array(stride),
-                                    int(bool(discrete)), _dt(data_type), int(device), r0, r1,
+                                    int(bool(discrete)), _dt(data_type), _enc(encoding),
+                                    int(device), r0, r1,
                                     int(nthreads), _flags(erase, finish), ctypes.byref(st)))
     return st.as_dict()
 
@@ -172,12 +213,13 @@ def _sigma_half(sigma, kernel_half_size):
 
 def gaussian(input_path, output_path, sigma, kernel_half_size, data_type: Optional[str] = None,
              device: int = 0, rows=None, nthreads: int = 0, erase: bool = True,
-             finish: bool = True) -> dict:
+             finish: bool = True, encoding=None) -> dict:
     """zarrs_filter gaussian INPUT OUTPUT SIGMA KERNEL_HALF_SIZE [--data-type T]."""
     st = _abi.StoreStats()
     r0, r1 = (0, -1) if rows is None else (int(rows[0]), int(rows[1]))
     sg, hs = _sigma_half(sigma, kernel_half_size)
-    check(lib().zt_store_gaussian(_b(input_path), _b(output_path), _dt(data_type), sg, hs,
+    check(lib().zt_store_gaussian(_b(input_path), _b(output_path), _dt(data_type),
+                                  _enc(encoding), sg, hs,
                                   int(device), r0, r1, int(nthreads), _flags(erase, finish),
                                   ctypes.byref(st)))
     return st.as_dict()
@@ -185,13 +227,15 @@ def gaussian(input_path, output_path, sigma, kernel_half_size, data_type: Option
 
 def downsample_gaussian(input_path, output_path, stride, sigma, kernel_half_size,
                         data_type: Optional[str] = None, device: int = 0, rows=None,
-                        nthreads: int = 0, erase: bool = True, finish: bool = True) -> dict:
+                        nthreads: int = 0, erase: bool = True, finish: bool = True,
+                        encoding=None) -> dict:
     """One zarrs_ome level with --gaussian-sigma (zarrs_ome.rs:236-271)."""
     st = _abi.StoreStats()
     r0, r1 = (0, -1) if rows is None else (int(rows[0]), int(rows[1]))
     sg, hs = _sigma_half(sigma, kernel_half_size)
     check(lib().zt_store_downsample_gaussian(_b(input_path), _b(output_path), i64_array(stride),
-                                             sg, hs, _dt(data_type), int(device), r0, r1,
+                                             sg, hs, _dt(data_type), _enc(encoding),
+                                             int(device), r0, r1,
                                              int(nthreads), _flags(erase, finish),
                                              ctypes.byref(st)))
     return st.as_dict()

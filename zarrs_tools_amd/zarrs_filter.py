@@ -14,13 +14,22 @@ accelerates:
 * a JSON run config is a list of {"filter": "guided_filter" | "downsample", "input", "output",
   ...args, "data_type"}, with "$name" meaning a named temporary array under --tmp and an omitted
   input meaning the previous filter's output (zarrs_filter.rs:106-138, :338-381);
+* every filter takes the reencoding arguments (ZarrReencodingArgs, lib.rs:274-377: -d/--data-type,
+  -f/--fill-value, --separator, -c/--chunk-shape, -s/--shard-shape, --array-to-array-codecs,
+  --array-to-bytes-codec, --bytes-to-bytes-codecs, --dimension-names, --attributes,
+  --attributes-append; the same snake_case keys in a run config), applied to the output array as
+  get_array_builder_reencode does (lib.rs:408-650; host/zt_store.cpp build_output);
 * `--exists erase` (default) overwrites an existing output, `exit` refuses it (:228-235);
-* the output metadata is erased before a filter runs and written when it finishes (:297-313).
+* the output metadata is erased before a filter runs and written when it finishes (:297-313);
+* per-chunk progress (Progress, progress.rs:15-119) is shown on a terminal as
+  `step/steps rw:READ/WRITE p:PROCESS` (thread-seconds, device seconds), like zarrs_filter.rs:
+  149-172.
 
 Filters outside the accelerated path (reencode, crop, rescale, clamp, equal, replace_value,
 gradient_magnitude, summed_area_table) are rejected with FilterError::Other: they are out of scope
-(DESIGN.md §1). `--chunk-limit` sets the number of host worker threads that decode and encode
-chunks (the reference's bound on concurrently processed chunks).
+(DESIGN.md §1). `--chunk-limit` bounds the chunks decoded / encoded at once (host worker
+threads); the chunk rows held in memory are bounded by 80 % of the available host and device
+memory, failing like calculate_chunk_limit (filter.rs:52-66) when not even one row fits.
 """
 from __future__ import annotations
 
@@ -46,6 +55,59 @@ def _parse_floats(s: str):
     return [float(x) for x in s.split(",") if x.strip()]
 
 
+# ZarrReencodingArgs (lib.rs:274-377), flattened into every filter's arguments
+# (filter_common_arguments.rs:7-16) and into the JSON run config (serde flatten).
+REENCODE_KEYS = ("data_type", "fill_value", "separator", "chunk_shape", "shard_shape",
+                 "array_to_array_codecs", "array_to_bytes_codec", "bytes_to_bytes_codecs",
+                 "dimension_names", "attributes", "attributes_append")
+
+
+def _parse_fill_value(s: str):
+    """parse_fill_value: JSON (0, 100, -1.5, "NaN", "[0, 255]"), else the bare string."""
+    if s in ("NaN", "Infinity", "-Infinity"):
+        return s  # the Zarr V3 fill-value strings, kept as strings
+    try:
+        return json.loads(s)
+    except ValueError:
+        return s
+
+
+def _add_reencode_args(p: argparse.ArgumentParser) -> None:
+    p.add_argument("-d", "--data-type", default=None)
+    p.add_argument("-f", "--fill-value", type=_parse_fill_value, default=None)
+    p.add_argument("--separator", default=None, choices=["/", "."])
+    p.add_argument("-c", "--chunk-shape", type=_parse_stride, default=None)
+    p.add_argument("-s", "--shard-shape", type=_parse_stride, default=None)
+    p.add_argument("--array-to-array-codecs", default=None)
+    p.add_argument("--array-to-bytes-codec", default=None)
+    p.add_argument("--bytes-to-bytes-codecs", default=None)
+    p.add_argument("--dimension-names", type=lambda s: s.split(","), default=None)
+    p.add_argument("--attributes", default=None)
+    p.add_argument("--attributes-append", default=None)
+    p.add_argument("--chunk-limit", dest="filter_chunk_limit", type=int, default=None)
+
+
+def _reencode_of(a) -> dict:
+    return {k: getattr(a, k) for k in REENCODE_KEYS if getattr(a, k, None) is not None}
+
+
+def encoding_of(step: dict) -> dict | None:
+    """The reencoding arguments of a run-config step (JSON strings of the codec / attribute
+    arguments parsed), or None when it has none."""
+    enc = {}
+    for k in REENCODE_KEYS:
+        v = step.get(k)
+        if v is None:
+            continue
+        if k in ("array_to_array_codecs", "array_to_bytes_codec", "bytes_to_bytes_codecs",
+                 "attributes", "attributes_append") and isinstance(v, str):
+            v = json.loads(v)
+        if k in ("chunk_shape", "shard_shape") and isinstance(v, str):
+            v = _parse_stride(v)
+        enc[k] = v
+    return enc or None
+
+
 def build_parser() -> argparse.ArgumentParser:
     ap = argparse.ArgumentParser(prog="zarrs_filter",
                                  description="Apply filters to a Zarr V3 array on an MI355X.")
@@ -60,22 +122,19 @@ def build_parser() -> argparse.ArgumentParser:
     g.add_argument("output")
     g.add_argument("epsilon", type=float)
     g.add_argument("radius", type=int)
-    g.add_argument("--data-type", default=None)
-    g.add_argument("--chunk-limit", dest="filter_chunk_limit", type=int, default=None)
+    _add_reencode_args(g)
     d = sub.add_parser("downsample", help="Downsample an image given a stride.")
     d.add_argument("input")
     d.add_argument("output")
     d.add_argument("stride", type=_parse_stride)
     d.add_argument("--discrete", action="store_true")
-    d.add_argument("--data-type", default=None)
-    d.add_argument("--chunk-limit", dest="filter_chunk_limit", type=int, default=None)
+    _add_reencode_args(d)
     gs = sub.add_parser("gaussian", help="Apply a Gaussian kernel.")
     gs.add_argument("input")
     gs.add_argument("output")
     gs.add_argument("sigma", type=_parse_floats)
     gs.add_argument("kernel_half_size", type=_parse_stride)
-    gs.add_argument("--data-type", default=None)
-    gs.add_argument("--chunk-limit", dest="filter_chunk_limit", type=int, default=None)
+    _add_reencode_args(gs)
     return ap
 
 
@@ -83,15 +142,15 @@ def _steps_from_cli(a) -> list:
     if a.filter == "guided-filter":
         return [{"filter": "guided_filter", "input": a.input, "output": a.output,
                  "epsilon": a.epsilon, "radius": a.radius, "data_type": a.data_type,
-                 "chunk_limit": a.filter_chunk_limit}]
+                 "chunk_limit": a.filter_chunk_limit, **_reencode_of(a)}]
     if a.filter == "downsample":
         return [{"filter": "downsample", "input": a.input, "output": a.output,
                  "stride": a.stride, "discrete": a.discrete, "data_type": a.data_type,
-                 "chunk_limit": a.filter_chunk_limit}]
+                 "chunk_limit": a.filter_chunk_limit, **_reencode_of(a)}]
     if a.filter == "gaussian":
         return [{"filter": "gaussian", "input": a.input, "output": a.output, "sigma": a.sigma,
                  "kernel_half_size": a.kernel_half_size, "data_type": a.data_type,
-                 "chunk_limit": a.filter_chunk_limit}]
+                 "chunk_limit": a.filter_chunk_limit, **_reencode_of(a)}]
     return []
 
 
@@ -123,6 +182,14 @@ def run(steps: list, exists: str = "erase", tmp: str | None = None,
         return p
 
     t_all = time.perf_counter()
+    if sys.stderr.isatty():
+        def _show(p):
+            sys.stderr.write(f"\r  {p['step']}/{p['num_steps']} rw:{p['read_s']:.2f}/"
+                             f"{p['write_s']:.2f} p:{p['process_s']:.3f}")
+            if p["step"] == p["num_steps"]:
+                sys.stderr.write("\n")
+            sys.stderr.flush()
+        S.set_progress_callback(_show)
     try:
         for i, step in enumerate(steps):
             name = step.get("filter")
@@ -148,7 +215,7 @@ def run(steps: list, exists: str = "erase", tmp: str | None = None,
                     f"{src} ({info.data_type} {list(info.shape)}) -> {dst}")
                 st = S.guided_filter(src, dst, float(step["epsilon"]), int(step["radius"]),
                                      data_type=step.get("data_type"), device=device,
-                                     nthreads=threads)
+                                     nthreads=threads, encoding=encoding_of(step))
             elif name == "gaussian":
                 sigma, half = step.get("sigma"), step.get("kernel_half_size")
                 if isinstance(sigma, str):
@@ -163,7 +230,7 @@ def run(steps: list, exists: str = "erase", tmp: str | None = None,
                 log(f"{i}: gaussian sigma={sigma} kernel_half_size={half} "
                     f"{src} ({info.data_type} {list(info.shape)}) -> {dst}")
                 st = S.gaussian(src, dst, sigma, half, data_type=step.get("data_type"),
-                                device=device, nthreads=threads)
+                                device=device, nthreads=threads, encoding=encoding_of(step))
             else:
                 stride = step.get("stride")
                 if isinstance(stride, str):
@@ -175,7 +242,7 @@ def run(steps: list, exists: str = "erase", tmp: str | None = None,
                     f"{src} ({info.data_type} {list(info.shape)}) -> {dst}")
                 st = S.downsample(src, dst, stride, discrete=bool(step.get("discrete", False)),
                                   data_type=step.get("data_type"), device=device,
-                                  nthreads=threads)
+                                  nthreads=threads, encoding=encoding_of(step))
             out = S.open_array(dst)
             log(f"   -> {out.data_type} {list(out.shape)} in {st['wall_s']:.2f}s "
                 f"(rw:{st['decode_s']:.2f}/{st['encode_s']:.2f} p:{st['kernel_s']:.3f})")
@@ -184,6 +251,8 @@ def run(steps: list, exists: str = "erase", tmp: str | None = None,
             results.append(st)
             last_output = dst
     finally:
+        if sys.stderr.isatty():
+            S.set_progress_callback(None)
         for d in made:
             shutil.rmtree(d, ignore_errors=True)
     log(f"Completed in {time.perf_counter() - t_all:.2f}s")

@@ -2,19 +2,32 @@
 array, every level computed by the HIP downsample kernel over the store.
 
     python -m zarrs_tools_amd.zarrs_ome INPUT OUTPUT [FACTOR,...] [--max-levels N] [--discrete]
-        [--gaussian-sigma S,...] [--gaussian-kernel-half-size H,...] [--device D]
-        [--chunk-limit N] [--name NAME]
+        [--gaussian-sigma S,...] [--gaussian-kernel-half-size H,...] [--physical-size P,...]
+        [--physical-units U,...] [--name NAME] [--group-attributes JSON]
+        [--exists erase|exit|overwrite] [--ome-zarr-version 0.5] [reencoding args]
+        [--device D] [--chunk-limit N]
 
-Follows src/bin/zarrs_ome.rs (0.7.2): level 0 is a copy of the input (:341-366, no reencoding);
-level i is the downsample of level i-1 read back from the output (:515-738) with the output chunk
-shape min(input chunk, output shape) (:549-559); the loop stops when every axis has factor 1 or
-extent 1 (:731-737); each level adds a multiscales dataset with scale = the cumulative factor and
-translation (scale - 1) / 2 (:716-726). Mean downsampling, the mode with --discrete (ties by
-the smallest value: the documented deviation), or with --gaussian-sigma a Gaussian
-of each level's input before the mean (apply_chunk_continuous_gaussian, :236-271; kernel half
-size default ceil(3 sigma), :494-502; ignored with --discrete, :638-646). The multiscales
-"type" is "mode", "average" or "gaussian" (:468-475); axes are named by the array's dimension
-names, else by index (:431-449).
+Follows src/bin/zarrs_ome.rs (0.7.2):
+* the output group gets --group-attributes (:317-323); --exists erase / exit / overwrite (:326-339);
+* level 0 is a copy of the input, or with any reencoding argument (ZarrReencodingArgs,
+  lib.rs:274-377) the input reencoded into the new encoding (:341-366);
+* array 0's attributes move to the group, without "_zarrs" (:368-377);
+* level i is the downsample of level i-1 read back from the output (:515-738). Its encoding is the
+  input's with zarrs_ome's per-level shapes (:528-560): a sharded input gets the shard shape
+  min(shard, output) and the inner chunk min(inner chunk, output); otherwise the chunk shape
+  min(chunk, output), which get_array_builder_reencode applies only to sharded outputs
+  (lib.rs:623-646), so an unsharded level keeps the input's chunk grid. The loop stops when every
+  axis has factor 1 or extent 1 (:731-737);
+* each level adds a dataset with the cumulative f32 scale of input/output shape ratios and
+  translation (scale - 1) / 2 (:570-578, :716-726);
+* axes are named by the array's dimension names, else by index, typed by --physical-units (space,
+  time, "channel", or a custom unit, :379-446); --physical-size is the multiscale's
+  coordinateTransformations (:448-452); the multiscales "type" is "mode", "average" or "gaussian"
+  (:468-475).
+Mean downsampling, the mode with --discrete (ties by the smallest value: the documented deviation,
+DESIGN.md §2), or with --gaussian-sigma a Gaussian of each level's input before the mean
+(apply_chunk_continuous_gaussian, :236-271; kernel half size default ceil(3 sigma), :494-502;
+ignored with --discrete, :638-646).
 """
 from __future__ import annotations
 
@@ -30,6 +43,21 @@ import numpy as np
 
 from . import _abi
 from . import store as S
+from .zarrs_filter import REENCODE_KEYS, _add_reencode_args, encoding_of
+
+VERSION = "zarrs_tools_amd 0.2 (MI355X)"
+
+# OME-NGFF 0.5 units (ome_zarr_metadata 0.2.3 AxisUnit: Space | Time | Custom)
+SPACE_UNITS = {
+    "angstrom", "attometer", "centimeter", "decimeter", "exameter", "femtometer", "foot",
+    "gigameter", "hectometer", "inch", "kilometer", "megameter", "meter", "micrometer", "mile",
+    "millimeter", "nanometer", "parsec", "petameter", "picometer", "terameter", "yard",
+    "yoctometer", "yottameter", "zeptometer", "zettameter"}
+TIME_UNITS = {
+    "attosecond", "centisecond", "day", "decisecond", "exasecond", "femtosecond", "gigasecond",
+    "hectosecond", "hour", "kilosecond", "megasecond", "microsecond", "millisecond", "minute",
+    "nanosecond", "petasecond", "picosecond", "second", "terasecond", "yoctosecond",
+    "yottasecond", "zeptosecond", "zettasecond"}
 
 
 def build_parser() -> argparse.ArgumentParser:
@@ -38,16 +66,21 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("output")
     ap.add_argument("factor", nargs="?", default=None,
                     type=lambda s: [int(x) for x in s.split(",")])
+    ap.add_argument("--ome-zarr-version", default="0.5", choices=["0.5"])
     ap.add_argument("--max-levels", type=int, default=10)
+    ap.add_argument("--physical-size", default=None,
+                    type=lambda s: [float(x) for x in s.split(",")])
+    ap.add_argument("--physical-units", default=None, type=lambda s: s.split(","))
     ap.add_argument("--discrete", action="store_true")
     ap.add_argument("--gaussian-sigma", default=None,
                     type=lambda s: [float(x) for x in s.split(",")])
     ap.add_argument("--gaussian-kernel-half-size", default=None,
                     type=lambda s: [int(x) for x in s.split(",")])
     ap.add_argument("--name", default=None)
-    ap.add_argument("--exists", choices=["erase", "exit"], default="erase")
+    ap.add_argument("--group-attributes", default=None)
+    ap.add_argument("--exists", choices=["erase", "exit", "overwrite"], default="erase")
     ap.add_argument("--device", type=int, default=0)
-    ap.add_argument("--chunk-limit", type=int, default=0)
+    _add_reencode_args(ap)  # adds --chunk-limit too
     return ap
 
 
@@ -64,9 +97,49 @@ def level_translation(scale):
     return [float(f32(f32(f32(s) - f32(1.0)) * f32(0.5))) for s in scale]
 
 
+def level_encoding(info: "S.ArrayInfo", out_shape) -> dict:
+    """zarrs_ome.rs:528-560: the per-level chunk (and shard) shape of level i from level i-1."""
+    if info.chunk_shape != info.inner_chunk_shape:  # sharded input
+        return {"shard_shape": [min(c, s) for c, s in zip(info.chunk_shape, out_shape)],
+                "chunk_shape": [min(g, s) for g, s in zip(info.inner_chunk_shape, out_shape)]}
+    return {"chunk_shape": [min(c, s) for c, s in zip(info.chunk_shape, out_shape)]}
+
+
+def axis_of(name: str, unit):
+    """units_to_axis (zarrs_ome.rs:390-432)."""
+    if unit is None:
+        return {"name": name}
+    if unit in SPACE_UNITS:
+        return {"name": name, "type": "space", "unit": unit}
+    if unit in TIME_UNITS:
+        return {"name": name, "type": "time", "unit": unit}
+    if unit == "channel":
+        return {"name": name, "type": "channel"}
+    return {"name": name, "unit": unit}
+
+
+def _reencode_level0(src, dst, encoding, nthreads, log):
+    """Reencode::apply for level 0: the input's data in the new encoding, chunk row by chunk row
+    (host copy through the store codecs)."""
+    S.create_output_like(src, dst, encoding.get("data_type"), encoding)
+    out = S.open_array(dst)
+    info = S.open_array(src)
+    cz = out.chunk_shape[0]
+    for z0 in range(0, info.shape[0], cz):
+        n = min(cz, info.shape[0] - z0)
+        block = S.read_array(src, [z0] + [0] * (info.ndim - 1), [n] + list(info.shape[1:]),
+                             nthreads=nthreads)
+        if out.data_type != info.data_type:
+            raise _abi.InvalidParameters(_abi.ERR_INVALID_PARAMETERS,
+                                         "zarrs_ome level 0: --data-type is not supported")
+        S.write_array(dst, block, [z0] + [0] * (info.ndim - 1), nthreads=nthreads)
+    log(f"0: reencode {src} -> {dst} ({out.data_type} {list(out.shape)})")
+
+
 def run(input_path, output_path, factor=None, max_levels: int = 10, discrete: bool = False,
         name=None, exists: str = "erase", device: int = 0, nthreads: int = 0,
-        gaussian_sigma=None, gaussian_kernel_half_size=None, log=print) -> dict:
+        gaussian_sigma=None, gaussian_kernel_half_size=None, physical_size=None,
+        physical_units=None, group_attributes=None, reencoding=None, log=print) -> dict:
     t0 = time.perf_counter()
     info = S.open_array(input_path)
     nd = info.ndim
@@ -83,30 +156,58 @@ def run(input_path, output_path, factor=None, max_levels: int = 10, discrete: bo
             raise _abi.InvalidParameters(_abi.ERR_INVALID_PARAMETERS,
                                          "gaussian sigma / kernel half size must match the rank")
         gauss = (sigma, half)
+    for what, v in (("physical size", physical_size), ("physical units", physical_units)):
+        if v is not None and len(v) != nd:
+            raise _abi.InvalidParameters(_abi.ERR_INVALID_PARAMETERS,
+                                         f"{what} must have one entry per axis")
+    group_attrs = {}
+    if group_attributes:
+        group_attrs.update(json.loads(group_attributes) if isinstance(group_attributes, str)
+                           else group_attributes)
     if os.path.exists(output_path):
         if exists == "exit":
-            raise _abi.FilterError(_abi.ERR_OTHER, f"output {output_path} already exists")
-        shutil.rmtree(output_path)
-    os.makedirs(output_path)
-    shutil.copytree(input_path, os.path.join(output_path, "0"))
-    log(f"0: copy {input_path} -> {output_path}/0 ({info.data_type} {list(info.shape)})")
+            raise _abi.FilterError(_abi.ERR_OTHER, "Output exists, exiting")
+        if exists == "erase":
+            shutil.rmtree(output_path)
+    os.makedirs(output_path, exist_ok=True)
+    lvl0 = os.path.join(output_path, "0")
+    if reencoding:
+        _reencode_level0(input_path, lvl0, reencoding, nthreads, log)
+    else:
+        if os.path.exists(lvl0):
+            shutil.rmtree(lvl0)
+        shutil.copytree(input_path, lvl0)
+        log(f"0: copy {input_path} -> {lvl0} ({info.data_type} {list(info.shape)})")
+    # move array 0's attributes to the group (zarrs_ome.rs:368-377)
+    meta0_path = os.path.join(lvl0, "zarr.json")
+    with open(meta0_path) as f:
+        meta0 = json.load(f)
+    moved = dict(meta0.get("attributes") or {})
+    moved.pop("_zarrs", None)
+    group_attrs.update(moved)
+    meta0["attributes"] = {}
+    with open(meta0_path, "w") as f:
+        json.dump(meta0, f, indent=2)
+    dim_names = meta0.get("dimension_names")
+
     scale = [1.0] * nd
     datasets = [{"path": "0", "coordinateTransformations": [
         {"type": "scale", "scale": list(scale)}]}]
-    shape = list(info.shape)
+    shape = list(S.open_array(lvl0).shape)
     stats = []
     for i in range(1, max_levels + 1):
         src, dst = os.path.join(output_path, str(i - 1)), os.path.join(output_path, str(i))
+        src_info = S.open_array(src)
+        out_shape = [max(s // f, 1) for s, f in zip(shape, factor)]  # downsample.rs:162-168
+        enc = level_encoding(src_info, out_shape)
         if gauss is not None:
             st = S.downsample_gaussian(src, dst, factor, gauss[0], gauss[1], device=device,
-                                       nthreads=nthreads)
+                                       nthreads=nthreads, encoding=enc)
         else:
             st = S.downsample(src, dst, factor, discrete=discrete, device=device,
-                              nthreads=nthreads)
+                              nthreads=nthreads, encoding=enc)
         stats.append(st)
         out = S.open_array(dst)
-        # zarrs_ome.rs:570-578: the real factor is input_shape / output_shape (integer division),
-        # accumulated into an f32 scale; translation (s - 1) * 0.5 in f32 (:716-723)
         scale = level_scale(scale, shape, out.shape)
         datasets.append({"path": str(i), "coordinateTransformations": [
             {"type": "scale", "scale": list(scale)},
@@ -115,19 +216,22 @@ def run(input_path, output_path, factor=None, max_levels: int = 10, discrete: bo
         shape = list(out.shape)
         if all(f == 1 or s == 1 for f, s in zip(factor, shape)):
             break
-    names = info.dimension_names if getattr(info, "dimension_names", None) else None
-    axes = [{"name": (names[k] if names and names[k] is not None else str(k))}
-            for k in range(nd)]
-    group = {"zarr_format": 3, "node_type": "group", "attributes": {"ome": {
-        "version": "0.5",
-        "multiscales": [{"name": name or os.path.basename(os.path.normpath(input_path)),
-                         "axes": axes, "datasets": datasets,
-                         "type": "mode" if discrete else ("average" if gauss is None
-                                                          else "gaussian"),
-                         "metadata": {"description": "Created with zarrs_tools_amd zarrs_ome",
-                                      "kwargs": {"factor": factor, "discrete": discrete,
-                                                 "gaussian_sigma": None if gauss is None
-                                                 else gauss[0]}}}]}}}
+    units = physical_units or [None] * nd
+    axes = [axis_of(dim_names[k] if dim_names and dim_names[k] is not None else str(k),
+                    units[k]) for k in range(nd)]
+    ms = {}
+    if name is not None:
+        ms["name"] = name
+    ms["axes"] = axes
+    ms["datasets"] = datasets
+    if physical_size is not None:
+        ms["coordinateTransformations"] = [{"type": "scale",
+                                            "scale": [float(x) for x in physical_size]}]
+    ms["type"] = "mode" if discrete else ("average" if gauss is None else "gaussian")
+    ms["metadata"] = {"description": "Created with zarrs_ome", "repository": "zarrs_tools_amd",
+                      "version": VERSION}
+    group_attrs["ome"] = {"version": "0.5", "multiscales": [ms]}
+    group = {"zarr_format": 3, "node_type": "group", "attributes": group_attrs}
     with open(os.path.join(output_path, "zarr.json"), "w") as f:
         json.dump(group, f, indent=2)
     log(f"Output {output_path} in {time.perf_counter() - t0:.2f}s")
@@ -136,9 +240,11 @@ def run(input_path, output_path, factor=None, max_levels: int = 10, discrete: bo
 
 def main(argv=None) -> int:
     a = build_parser().parse_args(argv)
+    enc = encoding_of({k: getattr(a, k, None) for k in REENCODE_KEYS})
     try:
         run(a.input, a.output, a.factor, a.max_levels, a.discrete, a.name, a.exists, a.device,
-            a.chunk_limit, a.gaussian_sigma, a.gaussian_kernel_half_size)
+            a.filter_chunk_limit or 0, a.gaussian_sigma, a.gaussian_kernel_half_size,
+            a.physical_size, a.physical_units, a.group_attributes, enc)
     except _abi.FilterError as e:
         print(f"Error: {e}", file=sys.stderr)
         return 1
