@@ -103,7 +103,9 @@ def test_downsample_store(tmp_path, discrete):
     ref = O.downsample(u, "uint16", (2, 2, 2), "uint16", discrete=discrete)
     np.testing.assert_array_equal(out, ref)
     info = S.open_array(tmp_path / "out")
-    assert info.shape == (18, 15, 22) and info.chunk_shape == (16, 15, 16)
+    # output_shape = max(n / s, 1); the chunk grid is the input's (Downsample::output_array_builder
+    # -> get_array_builder_reencode keeps the input's grid without sharding, lib.rs:623-646)
+    assert info.shape == (18, 15, 22) and info.chunk_shape == (16, 16, 16)
 
 
 def test_downsample_store_mixed_stride_float_out(tmp_path):

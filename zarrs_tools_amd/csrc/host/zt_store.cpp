@@ -641,8 +641,8 @@ void run_pipeline(const Array& in, const Array& out, int device, int64_t row_beg
                                            out_row_st.data());
                 bytes_written += n;
                 enc_ns += (int64_t)(secs_since(t0) * 1e9);
-                const int64_t step = ++chunks_done;  // Progress::next (progress.rs:101-104)
                 std::lock_guard<std::mutex> lk(g_progress_mu);
+                const int64_t step = ++chunks_done;  // Progress::next (progress.rs:101-104)
                 if (g_progress_fn) {
                     zt_progress pr{};
                     pr.step = step;
