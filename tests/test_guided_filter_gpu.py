@@ -252,3 +252,29 @@ def test_separable_4d_chunk_grid_subset(r):
     mask = np.ones(v.shape, bool)
     mask[box] = False
     assert np.all(out[mask] == -1)
+
+
+# ---- 4-D path (guided4d.hip: t-window sums of per-timepoint 3-D box sums), config T ----------
+
+@pytest.mark.parametrize("din,dout", [("uint16", "float32"), ("float32", "uint8"),
+                                      ("int16", "float64"), ("float32", "bfloat16")])
+def test_guided4d_element_types(din, dout):
+    rng = np.random.default_rng(41)
+    v32 = (rng.random((5, 9, 14, 70), dtype=np.float32) * 200).astype(np.float32)
+    v = O.cast_from_f32(v32, din)
+    chunk = (2, 4, 8, 32)
+    ref = O.guided_filter_apply(O.cast_to_f32(v, din), chunk, 300.0, 2, nthreads=8)
+    out = gpu_apply(v, din, dout, chunk, 300.0, 2)
+    check_against(out, ref, dout)
+
+
+@pytest.mark.parametrize("r", [1, 2, 4, 6])
+def test_guided4d_per_chunk_and_small_eps(r):
+    rng = np.random.default_rng(7 + r)
+    shape = (int(rng.integers(2, 9)), int(rng.integers(5, 20)), int(rng.integers(5, 30)),
+             int(rng.integers(5, 90)))
+    chunk = tuple(int(rng.integers(2, 9)) for _ in range(4))
+    v = (rng.random(shape, dtype=np.float32) * 300).astype(np.float32)
+    ref = O.guided_filter_apply(v, chunk, 0.5, r, nthreads=8)
+    assert rel_err(gpu_apply(v, "float32", "float32", chunk, 0.5, r), ref) <= FLOAT_TOL
+    assert rel_err(gpu_apply_chunked(v, "float32", "float32", chunk, 0.5, r), ref) <= FLOAT_TOL

@@ -1,0 +1,312 @@
+// guided4d.hip — the 4-D guided filter (config T: a (T, Z, Y, X) time series, every axis windowed
+// alike, guided_filter.rs:117-199 with get_block clamping on all four axes).
+//
+// The box mean over (t, z, y, x) is separable and linear, so the 4-D sums are t-window sums of
+// per-timepoint 3-D box sums:  box4(f)(t) = sum_{t' in W(t)} box3(f(t')).  Four kernels over the
+// halo'd block (windows clamp at the block bounds = the array bounds):
+//   K1 box3_march<float -> double>:  U3(t) = 3-D window sums of v, exact f64 (f64 sums of f32
+//       values), one z-march per (timepoint, xy tile);
+//   K2 pointwise (all t of a voxel in one thread): U4 = t-window sums of U3 (exact),
+//       u = RN(RN_f32(U4) / c4), s = (v-u)^2, a = s/(s+eps), b = (1-a)u  ->  AB (float2);
+//   K3 box3_march<float2 -> float2>: S3(t) = 3-D window sums of (a, b), f64 accumulation rounded
+//       to f32 once;
+//   K4 final (output region only): S4 = t-window sums of S3 (f64), mean = RN_f32(S4) / c4,
+//       out = RN(RN(v * mean_a) + mean_b) cast to TOut (guided_filter.rs:144-163, :101-102).
+// HBM traffic about 64 B per voxel (v read twice, U3 / AB / S3 written and read once) against the
+// separable path's ~160; every division is IEEE (correctly rounded), stage 1 exact, stage 2 with
+// f64 accumulation, so the result is closer to the reference's f64-SAT means than the 3-D kernel's.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "zt_device.hpp"
+#include "zt_kernels.hpp"
+
+namespace zt {
+
+namespace {
+
+struct dd2 {  // two f64 accumulators (the (a, b) pair)
+    double x, y;
+};
+
+__device__ __forceinline__ void acc_zero(double& a) { a = 0.0; }
+__device__ __forceinline__ void acc_zero(dd2& a) { a.x = a.y = 0.0; }
+__device__ __forceinline__ void acc_add(double& a, float v) { a += (double)v; }
+__device__ __forceinline__ void acc_sub(double& a, float v) { a -= (double)v; }
+__device__ __forceinline__ void acc_add(dd2& a, float2 v) { a.x += (double)v.x; a.y += (double)v.y; }
+__device__ __forceinline__ void acc_sub(dd2& a, float2 v) { a.x -= (double)v.x; a.y -= (double)v.y; }
+__device__ __forceinline__ void acc_add(double& a, double v) { a += v; }
+__device__ __forceinline__ void acc_sub(double& a, double v) { a -= v; }
+__device__ __forceinline__ void acc_add(dd2& a, const dd2& v) { a.x += v.x; a.y += v.y; }
+__device__ __forceinline__ void acc_sub(dd2& a, const dd2& v) { a.x -= v.x; a.y -= v.y; }
+__device__ __forceinline__ void put(double& o, double a) { o = a; }
+__device__ __forceinline__ void put(float2& o, const dd2& a) { o = make_float2((float)a.x, (float)a.y); }
+template <typename TV> __device__ __forceinline__ TV zero_v();
+template <> __device__ __forceinline__ float zero_v<float>() { return 0.0f; }
+template <> __device__ __forceinline__ float2 zero_v<float2>() { return make_float2(0.0f, 0.0f); }
+
+__device__ __forceinline__ int ccount(int i, int n, int r) {
+    const int lo = i - r < 0 ? 0 : i - r;
+    const int hi = i + r > n - 1 ? n - 1 : i + r;
+    return hi - lo + 1;
+}
+
+constexpr int kTX = 64, kTY = 16, kNT = 256, kKX = 4, kKY = 4;
+
+// 3-D window sums (radius R, clamped to the volume) of every timepoint volume of a (T, nz, ny, nx)
+// C-order array: a workgroup marches one 64 x 16 xy tile through zseg slices of one timepoint.
+// Each thread keeps the running z-window of its points of the (tile + R) apron in registers
+// (entering and leaving slices prefetched a step ahead); x- then y-window sums go through LDS.
+template <int R, typename TV, typename TA, typename TO>
+__global__ __launch_bounds__(kNT) void box3_march_kernel(const TV* __restrict__ in,
+                                                         TO* __restrict__ out, int nz, int ny,
+                                                         int nx, int zseg, int tiles_x,
+                                                         int tiles_y) {
+    constexpr int EX = kTX + 2 * R, EY = kTY + 2 * R, NE = EX * EY;
+    constexpr int NPT = (NE + kNT - 1) / kNT;
+    __shared__ TA Z[EY][EX];
+    __shared__ TA X[EY][kTX];
+    const int t = blockIdx.y;
+    const int ntile = tiles_x * tiles_y;
+    const int seg = blockIdx.x / ntile, tile = blockIdx.x % ntile;
+    const int x0 = (tile % tiles_x) * kTX, y0 = (tile / tiles_x) * kTY;
+    const int z0 = seg * zseg, z1 = min(z0 + zseg, nz);
+    const int64_t plane = (int64_t)ny * nx;
+    const TV* vol = in + (int64_t)t * nz * plane;
+    TO* ovol = out + (int64_t)t * nz * plane;
+
+    // owned apron points: index into the plane (or -1 outside the volume / past the apron)
+    int64_t pidx[NPT];
+    int ey_[NPT], ex_[NPT];
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+        const int e = threadIdx.x + k * kNT;
+        const int ey = e / EX, ex = e % EX;
+        const int gy = y0 - R + ey, gx = x0 - R + ex;
+        ey_[k] = e < NE ? ey : -1;
+        ex_[k] = ex;
+        pidx[k] = (e < NE && gy >= 0 && gy < ny && gx >= 0 && gx < nx) ? (int64_t)gy * nx + gx : -1;
+    }
+    auto load = [&](int z, int k) -> TV {
+        return (pidx[k] >= 0 && z >= 0 && z < nz) ? vol[(int64_t)z * plane + pidx[k]] : zero_v<TV>();
+    };
+    TA zs[NPT];
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {  // window of slice z0 - 1
+        acc_zero(zs[k]);
+        for (int z = z0 - 1 - R; z <= z0 - 1 + R; ++z) acc_add(zs[k], load(z, k));
+    }
+    TV pa[NPT], ps[NPT];
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+        pa[k] = load(z0 + R, k);
+        ps[k] = load(z0 - R - 1, k);
+    }
+    for (int z = z0; z < z1; ++z) {
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) {
+            acc_add(zs[k], pa[k]);
+            acc_sub(zs[k], ps[k]);
+            if (ey_[k] >= 0) Z[ey_[k]][ex_[k]] = zs[k];
+        }
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) {  // next step's entering / leaving slices
+            pa[k] = load(z + 1 + R, k);
+            ps[k] = load(z - R, k);
+        }
+        __syncthreads();
+        // x-window: EY rows x (kTX / kKX) segments of kKX outputs
+        for (int it = threadIdx.x; it < EY * (kTX / kKX); it += kNT) {
+            const int ey = it / (kTX / kKX), sx = (it % (kTX / kKX)) * kKX;
+            TA s;
+            acc_zero(s);
+#pragma unroll
+            for (int j = 0; j <= 2 * R; ++j) acc_add(s, Z[ey][sx + j]);
+            X[ey][sx] = s;
+#pragma unroll
+            for (int j = 1; j < kKX; ++j) {
+                acc_add(s, Z[ey][sx + j + 2 * R]);
+                acc_sub(s, Z[ey][sx + j - 1]);
+                X[ey][sx + j] = s;
+            }
+        }
+        __syncthreads();
+        // y-window: kTX columns x (kTY / kKY) segments; lanes on consecutive x (coalesced)
+        {
+            const int tx = threadIdx.x % kTX, sy = (threadIdx.x / kTX) * kKY;
+            const int gx = x0 + tx;
+            TA s;
+            acc_zero(s);
+#pragma unroll
+            for (int j = 0; j <= 2 * R; ++j) acc_add(s, X[sy + j][tx]);
+#pragma unroll
+            for (int j = 0; j < kKY; ++j) {
+                if (j > 0) {
+                    acc_add(s, X[sy + j + 2 * R][tx]);
+                    acc_sub(s, X[sy + j - 1][tx]);
+                }
+                const int gy = y0 + sy + j;
+                if (gx < nx && gy < ny) put(ovol[(int64_t)z * plane + (int64_t)gy * nx + gx], s);
+            }
+        }
+        // (the next step's Z writes come after every thread passed the barrier above, i.e.
+        //  after all x-window reads of Z; the next X writes follow its first barrier)
+    }
+}
+
+// K2: u, s, a, b for every timepoint of a voxel (guided_filter.rs:126-142) with 4-D counts.
+__global__ __launch_bounds__(256) void g4_pointwise_kernel(const double* __restrict__ U3,
+                                                           const float* __restrict__ v,
+                                                           float2* __restrict__ AB, int T,
+                                                           int nz, int ny, int nx, int r,
+                                                           float eps) {
+    const int64_t vol = (int64_t)nz * ny * nx;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < vol;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int x = (int)(i % nx);
+        const int64_t q = i / nx;
+        const int y = (int)(q % ny), z = (int)(q / ny);
+        const int c3 = ccount(z, nz, r) * ccount(y, ny, r) * ccount(x, nx, r);
+        for (int t = 0; t < T; ++t) {
+            double U4 = 0.0;
+            const int ta = max(t - r, 0), tb = min(t + r, T - 1);
+            for (int tt = ta; tt <= tb; ++tt) U4 += U3[tt * vol + i];
+            const float cnt = (float)(c3 * (tb - ta + 1));
+            const float u = (float)U4 / cnt;  // summed_area_table_mean: (sum as f32) / count
+            const float vv = v[t * vol + i];
+            const float d = vv - u;
+            const float s = d * d;  // (v - u).powf(2.0)
+            const float a = s / (s + eps);
+            const float b = (1.0f - a) * u;
+            AB[t * vol + i] = make_float2(a, b);
+        }
+    }
+}
+
+// K4: the output region [o0, o0 + on) of the block: t-window sums of S3, means, v*ma + mb.
+template <typename TOut>
+__global__ __launch_bounds__(256) void g4_final_kernel(const float2* __restrict__ S3,
+                                                       const float* __restrict__ v,
+                                                       TOut* __restrict__ out, NdGeom g, int r) {
+    const int T = (int)g.shape[0], nz = (int)g.shape[1], ny = (int)g.shape[2],
+              nx = (int)g.shape[3];
+    const int64_t vol = (int64_t)nz * ny * nx;
+    const int64_t on3 = g.out_shape[1] * g.out_shape[2] * g.out_shape[3];
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < on3;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int ox = (int)(i % g.out_shape[3]);
+        const int64_t q = i / g.out_shape[3];
+        const int oy = (int)(q % g.out_shape[2]), oz = (int)(q / g.out_shape[2]);
+        const int x = ox + (int)g.out_start[3], y = oy + (int)g.out_start[2],
+                  z = oz + (int)g.out_start[1];
+        const int64_t bi = ((int64_t)z * ny + y) * nx + x;
+        const int c3 = ccount(z, nz, r) * ccount(y, ny, r) * ccount(x, nx, r);
+        const int64_t dbase = oz * g.out_strides[1] + oy * g.out_strides[2] + ox * g.out_strides[3];
+        for (int ot = 0; ot < (int)g.out_shape[0]; ++ot) {
+            const int t = ot + (int)g.out_start[0];
+            const int ta = max(t - r, 0), tb = min(t + r, T - 1);
+            double sa = 0.0, sb = 0.0;
+            for (int tt = ta; tt <= tb; ++tt) {
+                const float2 p = S3[tt * vol + bi];
+                sa += (double)p.x;
+                sb += (double)p.y;
+            }
+            const float cnt = (float)(c3 * (tb - ta + 1));
+            const float ma = (float)sa / cnt, mb = (float)sb / cnt;
+            const float o = __fadd_rn(__fmul_rn(v[t * vol + bi], ma), mb);  // v *= ma; v += mb
+            out[dbase + ot * g.out_strides[0]] = from_f32<TOut>(o);
+        }
+    }
+}
+
+template <int R, typename TV, typename TA, typename TO>
+hipError_t launch_box3(const TV* in, TO* out, int T, int nz, int ny, int nx, hipStream_t s) {
+    const int tiles_x = (nx + kTX - 1) / kTX, tiles_y = (ny + kTY - 1) / kTY;
+    const int64_t tiles = (int64_t)tiles_x * tiles_y;
+    // z segments: enough workgroups for the chip (>= ~4 per CU), at least 16 slices each
+    int nseg = (int)std::max<int64_t>(1, std::min<int64_t>((nz + 15) / 16, (4096 + tiles * T - 1) / (tiles * T)));
+    const int zseg = (nz + nseg - 1) / nseg;
+    nseg = (nz + zseg - 1) / zseg;
+    const int64_t gx = tiles * nseg;
+    if (gx > 0x7FFFFFFF || T > 65535) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((box3_march_kernel<R, TV, TA, TO>), dim3((unsigned)gx, (unsigned)T),
+                       dim3(kNT), 0, s, in, out, nz, ny, nx, zseg, tiles_x, tiles_y);
+    return hipGetLastError();
+}
+
+template <typename TV, typename TA, typename TO>
+hipError_t launch_box3_r(int r, const TV* in, TO* out, int T, int nz, int ny, int nx,
+                         hipStream_t s) {
+    switch (r) {
+    case 1: return launch_box3<1, TV, TA, TO>(in, out, T, nz, ny, nx, s);
+    case 2: return launch_box3<2, TV, TA, TO>(in, out, T, nz, ny, nx, s);
+    case 3: return launch_box3<3, TV, TA, TO>(in, out, T, nz, ny, nx, s);
+    case 4: return launch_box3<4, TV, TA, TO>(in, out, T, nz, ny, nx, s);
+    case 5: return launch_box3<5, TV, TA, TO>(in, out, T, nz, ny, nx, s);
+    case 6: return launch_box3<6, TV, TA, TO>(in, out, T, nz, ny, nx, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace
+
+// radius <= 6: the f64-pair LDS tiles of K3 stay within 64 KB
+bool guided4d_supports(int radius) { return radius >= 1 && radius <= 6; }
+
+int64_t guided4d_scratch_bytes(int64_t numel, bool gather) {
+    // U3 / S3 (8 B) | AB (8 B) | v (4 B, when the input is not a contiguous f32 block)
+    return numel * (16 + (gather ? 4 : 0)) + 64;
+}
+
+hipError_t launch_guided4d(const void* in, int dtype_in, void* out, int dtype_out,
+                           const NdGeom& g, int radius, float eps, void* scratch, hipStream_t s) {
+    const int T = (int)g.shape[0], nz = (int)g.shape[1], ny = (int)g.shape[2],
+              nx = (int)g.shape[3];
+    const int64_t n = g.numel;
+    if (n <= 0 || g.out_numel <= 0) return hipSuccess;
+    char* base = static_cast<char*>(scratch);
+    double* U3 = reinterpret_cast<double*>(base);          // later S3 (float2) in place
+    float2* AB = reinterpret_cast<float2*>(base + n * 8);
+    bool contiguous = dtype_in == kF32;
+    {
+        int64_t st = 1;
+        for (int d = 3; d >= 0; --d) {
+            if (g.in_strides[d] != st) contiguous = false;
+            st *= g.shape[d];
+        }
+    }
+    const float* v = static_cast<const float*>(in);
+    hipError_t e;
+    if (!contiguous) {
+        float* vv = reinterpret_cast<float*>(base + n * 16);
+        for (int t = 0; t < T; ++t) {
+            const size_t esz = dtype_size(dtype_in);
+            e = launch_cast_to_f32_3d(static_cast<const char*>(in) + esz * t * g.in_strides[0],
+                                      dtype_in, g.in_strides[1], g.in_strides[2],
+                                      vv + (int64_t)t * nz * ny * nx, nz, ny, nx, s);
+            if (e != hipSuccess) return e;
+        }
+        v = vv;
+    }
+    e = launch_box3_r<float, double, double>(radius, v, U3, T, nz, ny, nx, s);
+    if (e != hipSuccess) return e;
+    const int64_t vol = (int64_t)nz * ny * nx;
+    const unsigned blocks = (unsigned)std::min<int64_t>((vol + 255) / 256, 256 * 64);
+    hipLaunchKernelGGL(g4_pointwise_kernel, dim3(blocks), dim3(256), 0, s, U3, v, AB, T, nz, ny,
+                       nx, radius, eps);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    float2* S3 = reinterpret_cast<float2*>(U3);
+    e = launch_box3_r<float2, dd2, float2>(radius, AB, S3, T, nz, ny, nx, s);
+    if (e != hipSuccess) return e;
+    const int64_t on3 = g.out_shape[1] * g.out_shape[2] * g.out_shape[3];
+    const unsigned oblocks = (unsigned)std::min<int64_t>((on3 + 255) / 256, 256 * 64);
+    e = hipErrorInvalidValue;
+    ZT_DISPATCH_DTYPE(dtype_out, TO,
+        hipLaunchKernelGGL(g4_final_kernel<TO>, dim3(oblocks), dim3(256), 0, s, S3, v,
+                           static_cast<TO*>(out), g, radius);
+        e = hipGetLastError())
+    return e;
+}
+
+}  // namespace zt

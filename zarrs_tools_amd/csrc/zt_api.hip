@@ -277,6 +277,37 @@ int run_separable(zt_ctx* ctx, int dtype_in, const void* in, const int64_t* shap
     return ZT_OK;
 }
 
+// 4-D blocks (config T): the four-kernel path of guided4d.hip when the radius fits it and x is
+// the unit-stride axis; the scratch holds U3/S3, AB and (for other element types or strides) f32 v.
+bool use_guided4d(int ndim, int radius, const int64_t* in_strides) {
+    return ndim == 4 && zt::guided4d_supports(radius) && in_strides[3] == 1;
+}
+
+int run_guided4d(zt_ctx* ctx, int dtype_in, const void* in, const int64_t* shape,
+                 const int64_t* in_strides, const int64_t* out_start, const int64_t* out_shape,
+                 int dtype_out, void* out, const int64_t* out_strides, float eps, int radius) {
+    zt::NdGeom g{};
+    g.ndim = 4;
+    g.numel = numel(shape, 4);
+    g.out_numel = numel(out_shape, 4);
+    for (int d = 0; d < 4; ++d) {
+        g.shape[d] = shape[d];
+        g.in_strides[d] = in_strides[d];
+        g.out_start[d] = out_start[d];
+        g.out_shape[d] = out_shape[d];
+        g.out_strides[d] = out_strides[d];
+        if (shape[d] > INT32_MAX) return fail(ZT_ERR_INVALID_PARAMETERS, "extent exceeds 2^31-1");
+    }
+    if (g.numel == 0 || g.out_numel == 0) return ZT_OK;
+    if (int rc = ctx->ensure_scratch((size_t)zt::guided4d_scratch_bytes(g.numel, true))) return rc;
+    if (ctx->timed) ZT_HIP(hipEventRecord(ctx->ev0, ctx->cur));
+    hipError_t e = zt::launch_guided4d(in, dtype_in, out, dtype_out, g, radius, eps,
+                                       ctx->scratch, ctx->cur);
+    if (e != hipSuccess) return hip_fail(e, "guided filter 4-D launch");
+    if (ctx->timed) ZT_HIP(hipEventRecord(ctx->ev1, ctx->cur));
+    return ZT_OK;
+}
+
 }  // namespace
 
 namespace zt {
@@ -480,6 +511,9 @@ int zt_guided_filter_apply_ndarray(zt_ctx* ctx, int dtype_in, const void* in,
             return run_fused3(ctx, dtype_in, in, dom, 0, dom[0], isz, isy, ost, osh, dtype_out,
                               out, osz, osy, epsilon, radius, 0);
     }
+    if (use_guided4d(ndim, radius, is))
+        return run_guided4d(ctx, dtype_in, in, in_shape, is, out_start, out_shape, dtype_out, out,
+                            os, epsilon, radius);
     return run_separable(ctx, dtype_in, in, in_shape, is, ndim, out_start, out_shape, dtype_out,
                          out, os, epsilon, radius);
 }
@@ -549,8 +583,10 @@ int zt_guided_filter_apply_array(zt_ctx* ctx, int dtype_in, const void* in, int 
         int rc = zt_subset_overlap(shape, ndim, ostart, oshape, ov, is0, ish, dst);
         if (rc) return rc;
         size_t free_b = 0, total_b = 0;
+        const bool g4 = use_guided4d(ndim, radius, strides);
         const size_t need =
-            sizeof(float) * (size_t)zt::separable_scratch_floats(numel(ish, ndim));
+            g4 ? (size_t)zt::guided4d_scratch_bytes(numel(ish, ndim), true)
+               : sizeof(float) * (size_t)zt::separable_scratch_floats(numel(ish, ndim));
         const bool have = ctx->scratch_bytes >= need ||
                           (hipMemGetInfo(&free_b, &total_b) == hipSuccess &&
                            need + ctx->scratch_bytes <= free_b / 2);
@@ -561,6 +597,11 @@ int zt_guided_filter_apply_array(zt_ctx* ctx, int dtype_in, const void* in, int 
                 ioff += is0[d] * strides[d];
                 ooff += ostart[d] * strides[d];
             }
+            if (g4)
+                return run_guided4d(ctx, dtype_in, static_cast<const char*>(in) + esz_in * ioff,
+                                    ish, strides, dst, oshape, dtype_out,
+                                    static_cast<char*>(out) + esz_out * ooff, strides, epsilon,
+                                    radius);
             return run_separable(ctx, dtype_in, static_cast<const char*>(in) + esz_in * ioff,
                                  ish, strides, ndim, dst, oshape, dtype_out,
                                  static_cast<char*>(out) + esz_out * ooff, strides, epsilon,
@@ -585,9 +626,15 @@ int zt_guided_filter_apply_array(zt_ctx* ctx, int dtype_in, const void* in, int 
             ioff += is0[d] * strides[d];
             ooff += cs[d] * strides[d];
         }
-        rc = run_separable(ctx, dtype_in, static_cast<const char*>(in) + esz_in * ioff, ish,
-                           strides, ndim, dst, csh, dtype_out,
-                           static_cast<char*>(out) + esz_out * ooff, strides, epsilon, radius);
+        rc = use_guided4d(ndim, radius, strides)
+                 ? run_guided4d(ctx, dtype_in, static_cast<const char*>(in) + esz_in * ioff, ish,
+                                strides, dst, csh, dtype_out,
+                                static_cast<char*>(out) + esz_out * ooff, strides, epsilon,
+                                radius)
+                 : run_separable(ctx, dtype_in, static_cast<const char*>(in) + esz_in * ioff, ish,
+                                 strides, ndim, dst, csh, dtype_out,
+                                 static_cast<char*>(out) + esz_out * ooff, strides, epsilon,
+                                 radius);
         if (rc) return rc;
     }
     return ZT_OK;

@@ -68,6 +68,12 @@ hipError_t launch_guided_separable(const void* in, int dtype_in, void* out, int 
                                    const NdGeom& g, int radius, float eps, float* scratch,
                                    hipStream_t s);
 
+// 4-D guided filter (guided4d.hip): t-window sums of per-timepoint 3-D box sums, four kernels.
+bool guided4d_supports(int radius);
+int64_t guided4d_scratch_bytes(int64_t numel, bool gather);
+hipError_t launch_guided4d(const void* in, int dtype_in, void* out, int dtype_out,
+                           const NdGeom& g, int radius, float eps, void* scratch, hipStream_t s);
+
 // Downsample (downsample.rs:72-120). g.shape = input shape, g.out_shape = output shape,
 // win = window per axis (min(stride, extent)).
 struct DSParams {
