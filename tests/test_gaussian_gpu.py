@@ -77,6 +77,51 @@ def test_all_output_types(dout):
     assert np.array_equal(out.view(np.uint8), want.view(np.uint8))
 
 
+# The fused z/y/x march (gaussian.hip gauss_zyx_kernel): one tap length L on the last three
+# axes, L in 3..13; several tiles, z segments and chunk-region offsets.
+@pytest.mark.parametrize("shape,chunk,sigma,half", [
+    ((19, 37, 70), (8, 16, 32), [0.6] * 3, [1] * 3),
+    ((70, 45, 150), (32, 32, 64), [1.0, 1.2, 0.9], [2, 2, 2]),
+    ((90, 66, 130), (64, 33, 65), [1.0] * 3, [3] * 3),
+    ((40, 35, 100), (16, 16, 32), [2.0] * 3, [4] * 3),
+    ((30, 40, 70), (30, 40, 70), [2.5] * 3, [5] * 3),
+    ((25, 31, 67), (7, 9, 11), [3.0] * 3, [6] * 3),
+    ((3, 9, 20, 70), (2, 5, 8, 32), [1.0, 1.0, 0.8, 1.1], [2, 3, 3, 3]),
+])
+def test_fused_zyx_march_bit_exact(shape, chunk, sigma, half):
+    rng = np.random.default_rng(sum(shape) + half[-1])
+    v = (rng.random(shape, dtype=np.float32) * 1000 - 200).astype(np.float32)
+    ref = O.gaussian_apply(v, chunk, sigma, half)
+    out = gpu_gaussian(v, "float32", "float32", chunk, sigma, half)
+    assert np.array_equal(out, ref)
+
+
+@pytest.mark.parametrize("din", ["uint8", "int16", "uint16", "float64"])
+def test_fused_zyx_march_input_types(din):
+    rng = np.random.default_rng(5)
+    v32 = (rng.random((20, 24, 72), dtype=np.float32) * 200 - (50 if din.startswith("int") else 0))
+    v = O.cast_from_f32(v32, din)
+    ref = O.gaussian_apply(O.cast_to_f32(v, din), (8, 16, 32), [1.0] * 3, [3] * 3)
+    out = gpu_gaussian(v, din, "float32", (8, 16, 32), [1.0] * 3, [3] * 3)
+    assert np.array_equal(out, ref)
+
+
+def test_fused_zyx_march_per_chunk():
+    import itertools
+    import torch
+    v = O.synth_step_noise_f32((40, 48, 100))
+    sigma, half, chunk = [1.0] * 3, [3] * 3, (16, 16, 32)
+    ref = O.gaussian_apply(v, chunk, sigma, half)
+    x = to_dev(v, "float32")
+    y = torch.empty(v.shape, device="cuda")
+    a_in, a_out = zt.DeviceArray(x, chunk), zt.DeviceArray(y, chunk)
+    g = zt.Gaussian(sigma, half)
+    for idx in itertools.product(*[range(n) for n in a_out.chunk_grid_shape()]):
+        g.apply_chunk(a_in, a_out, idx)
+    torch.cuda.synchronize()
+    assert np.array_equal(from_dev(y, "float32"), ref)
+
+
 @pytest.mark.parametrize("codec", ["bytes", "gzip"])
 def test_store_gaussian(tmp_path, codec):
     shape, chunk = (40, 36, 70), (16, 16, 32)

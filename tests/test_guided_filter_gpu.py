@@ -278,3 +278,49 @@ def test_guided4d_per_chunk_and_small_eps(r):
     ref = O.guided_filter_apply(v, chunk, 0.5, r, nthreads=8)
     assert rel_err(gpu_apply(v, "float32", "float32", chunk, 0.5, r), ref) <= FLOAT_TOL
     assert rel_err(gpu_apply_chunked(v, "float32", "float32", chunk, 0.5, r), ref) <= FLOAT_TOL
+
+
+# ---- 4-D one-march kernel (g4_fused.hip): T <= 4 timepoints per block, r <= 2 ---------------
+
+@pytest.mark.parametrize("shape,chunk,r", [
+    ((4, 40, 37, 150), (2, 16, 16, 64), 2),
+    ((3, 70, 20, 65), (3, 32, 8, 32), 2),
+    ((1, 33, 9, 130), (1, 8, 8, 64), 1),
+    ((2, 45, 26, 71), (1, 16, 13, 40), 1),
+    ((4, 12, 5, 7), (4, 4, 4, 4), 2),
+])
+def test_guided4d_fused_vs_oracle_small_eps(shape, chunk, r):
+    rng = np.random.default_rng(sum(shape) + r)
+    v = (rng.random(shape, dtype=np.float32) * 300).astype(np.float32)
+    ref = O.guided_filter_apply(v, chunk, 0.5, r, nthreads=8)
+    assert rel_err(gpu_apply(v, "float32", "float32", chunk, 0.5, r), ref) <= FLOAT_TOL
+    assert rel_err(gpu_apply_chunked(v, "float32", "float32", chunk, 0.5, r), ref) <= FLOAT_TOL
+
+
+@pytest.mark.parametrize("din,dout", [("uint16", "float32"), ("float32", "uint8"),
+                                      ("float64", "float16")])
+def test_guided4d_fused_element_types(din, dout):
+    rng = np.random.default_rng(43)
+    v32 = (rng.random((4, 20, 17, 70), dtype=np.float32) * 200).astype(np.float32)
+    v = O.cast_from_f32(v32, din)
+    chunk = (2, 8, 8, 32)
+    ref = O.guided_filter_apply(O.cast_to_f32(v, din), chunk, 300.0, 2, nthreads=8)
+    check_against(gpu_apply(v, din, dout, chunk, 300.0, 2), ref, dout)
+
+
+def test_guided4d_fused_chunk_grid_subset():
+    import torch
+    v = O.synth_step_noise_f32((4, 24, 16, 96))
+    chunk = (2, 8, 8, 32)
+    ref = O.guided_filter_apply(v, chunk, 2500.0, 2, nthreads=8)
+    x = to_dev(v, "float32")
+    y = torch.full(v.shape, -1.0, device="cuda")
+    zt.GuidedFilter(2500.0, 2).apply(zt.DeviceArray(x, chunk), zt.DeviceArray(y, chunk),
+                                     chunk_grid_start=(1, 1, 0, 1),
+                                     chunk_grid_count=(1, 2, 1, 2))
+    out = from_dev(y, "float32")
+    box = (slice(2, 4), slice(8, 24), slice(0, 8), slice(32, 96))
+    assert rel_err(out[box], ref[box]) <= FLOAT_TOL
+    mask = np.ones(v.shape, bool)
+    mask[box] = False
+    assert np.all(out[mask] == -1)

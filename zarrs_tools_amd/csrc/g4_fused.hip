@@ -1,0 +1,424 @@
+// g4_fused.hip — the 4-D guided filter in one z-march for blocks of at most 4 timepoints (config
+// T's per-GPU share): guided_filter.rs:117-164 with get_block clamping on all four axes
+// (:166-184), both stages and every timepoint of an xy tile in one workgroup, so v is read from
+// HBM about once and the output written once (against ~64 B per voxel for the four-kernel path
+// of guided4d.hip).
+//
+// A workgroup owns a 64 x 8 xy output tile for all T <= 4 timepoints and marches
+// z through a segment of output slices; stage 1 runs R slices ahead of stage 2. Per step, with
+// zc the stage-1 slice and zo = zc - R the output slice:
+//   S1  running z-window (f64, exact) of v on the (64+4R) x (8+4R) apron of every timepoint:
+//       + entering slice zc+R, - leaving slice zc-R-1                         -> Z1 (LDS, f64)
+//   S2  x-window sums of Z1 rows on the (64+2R) columns                          -> X1 (LDS, f64)
+//   S3  y-window sums -> U3(t) on the (64+2R) x (8+2R) apron; t-window sums -> U4 (exact);
+//       u = RN(RN_f32(U4) / c4), s = (v-u)^2, a = s/(s+eps), b = (1-a)u;
+//       zero outside the block (the clamped sums of stage 2)                   -> Lab (LDS, f32 x2)
+//   S4  x-window sums of (a, b) rows on the 64 tile columns                    -> Hab (LDS, f32 x2)
+//   S5  y-window sums + t-window sums of (a, b) -> P(zc), kept in an LDS history of the last
+//       2R+1 slices whose sum is the z-window;
+//       out(zo) = RN(RN(v * RN(S4a / c4)) + RN(S4b / c4)).
+// A workgroup has 1024 threads (4 waves per SIMD) and ~154 KB of LDS. Four LDS barriers per
+// step; Z1/Lab and X1/Hab share LDS (their lifetimes alternate). Stage 1 is exact like the 3-D
+// kernel's; stage 2's xy and t sums are f32 (the tolerance of DESIGN.md §4).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <type_traits>
+
+#include "zt_device.hpp"
+#include "zt_kernels.hpp"
+
+namespace zt {
+
+namespace {
+
+constexpr int kFTX = 64, kFTY = 8, kFTS = 4;  // tile width, height, timepoints per block
+
+template <int R>
+struct G4FConfig {
+    static constexpr int TX = kFTX, TY = kFTY, TS = kFTS, W = 2 * R + 1;
+    static constexpr int E2X = TX + 4 * R, E2Y = TY + 4 * R;  // stage-1 apron
+    static constexpr int E1X = TX + 2 * R, E1Y = TY + 2 * R;  // (a, b) apron
+    static constexpr int NT = 1024;  // one workgroup per CU, 4 waves per SIMD
+    static constexpr int NE2 = E2X * E2Y, NPT = (NE2 + NT - 1) / NT;  // S1 points per thread per t
+    static constexpr int PZ = ((E2X + 4 + 1) / 2) * 2;  // Z1 pitch (x-sum segments read past E2X)
+    static constexpr int KX2 = 4, NSX2 = (E1X + KX2 - 1) / KX2, NI2 = TS * E2Y * NSX2;
+    static constexpr int KY3 = 2, NSY3 = (E1Y + KY3 - 1) / KY3, NI3 = E1X * NSY3;
+    static constexpr int KX4 = 8, NI4 = TS * E1Y * (TX / KX4);
+    static constexpr int NI5 = TX * TY;
+    static constexpr int SZ_A = std::max<int>(TS * E2Y * PZ * 8, TS * E1Y * E1X * 8);
+    static constexpr int SZ_B = std::max<int>(TS * E2Y * E1X * 8, TS * E1Y * TX * 8);
+    static_assert(E1Y % KY3 == 0, "S3 segments tile the apron rows (X1 reads stay in E2Y)");
+    static constexpr int SZ_RING = W * TS * TY * TX * 8;  // stage-2 slice history (float2)
+    static constexpr int LDS = SZ_A + SZ_B + SZ_RING;
+    static_assert(NI3 <= NT && NI4 <= NT && NI5 <= NT, "one item per thread in S3-S5");
+    static_assert(TX % KX4 == 0, "S4 segments");
+    static_assert(LDS <= 160 * 1024, "LDS budget");
+};
+
+struct G4FParams {
+    const float* v;  // (T, nz, ny, nx) f32, C order (the halo'd block)
+    void* out;       // output region, strides os
+    int T, nz, ny, nx;
+    int o0[4], on[4];
+    int64_t os[4];
+    int zseg, tiles_x, tiles_y;
+    float eps;
+};
+
+__device__ __forceinline__ int fcount(int i, int n, int r) {
+    const int lo = i - r < 0 ? 0 : i - r;
+    const int hi = i + r > n - 1 ? n - 1 : i + r;
+    return hi - lo + 1;
+}
+
+// Buffer (SRD) loads: 32-bit byte offsets and the hardware range check (an offset past
+// num_records reads 0), so out-of-block points need no branch and no 64-bit address math.
+using rsrc_t = __amdgpu_buffer_rsrc_t;
+constexpr int kBad = (int)0x80000000;  // >= num_records of any slice: reads 0
+__device__ __forceinline__ rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+    // built from kernel arguments and loop counters only (wave-uniform): stays in SGPRs
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes,
+                                             0x00020000);
+}
+__device__ __forceinline__ float ldb(rsrc_t r, int off) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
+
+// Workgroup barrier for the LDS hand-offs only: __syncthreads() also fences global memory, which
+// would drain the loads kept in flight across it (the next slices' prefetches).
+__device__ __forceinline__ void lds_barrier() {
+    __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+template <int B, int E, typename F>
+__device__ __forceinline__ void sfor(F&& f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        sfor<B + 1, E>(f);
+    }
+}
+
+template <int R, typename TOut>
+__global__ __launch_bounds__(G4FConfig<R>::NT) void g4_fused_kernel(G4FParams p) {
+    using C = G4FConfig<R>;
+    constexpr int TX = C::TX, TY = C::TY, TS = C::TS, W = C::W, NT = C::NT, NPT = C::NPT;
+    constexpr int E2X = C::E2X, E2Y = C::E2Y, E1X = C::E1X, E1Y = C::E1Y, PZ = C::PZ;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    double* Z1 = reinterpret_cast<double*>(smem);                  // [TS][E2Y][PZ]
+    float2* Lab = reinterpret_cast<float2*>(smem);                 // [TS][E1Y][E1X]
+    double* X1 = reinterpret_cast<double*>(smem + C::SZ_A);        // [TS][E2Y][E1X]
+    float2* Hab = reinterpret_cast<float2*>(smem + C::SZ_A);       // [TS][E1Y][TX]
+    float2* Ring = reinterpret_cast<float2*>(smem + C::SZ_A + C::SZ_B);  // [W][TS][TY * TX]
+    const int tid = threadIdx.x;
+    const int T = p.T, nz = p.nz, ny = p.ny, nx = p.nx;
+    const int64_t plane = (int64_t)ny * nx, vol = (int64_t)nz * plane;
+
+    // XCD-aware block -> (tile, z segment): consecutive logical ids (x-adjacent tiles of one
+    // segment) share an XCD, whose L2 then holds the shared apron columns.
+    const int nwg = gridDim.x, b = blockIdx.x;
+    const int lid = (nwg % 8 == 0) ? (b % 8) * (nwg / 8) + b / 8 : b;
+    const int ntiles = p.tiles_x * p.tiles_y;
+    const int tile = lid % ntiles, seg = lid / ntiles;
+    const int x0 = p.o0[3] + (tile % p.tiles_x) * TX, y0 = p.o0[2] + (tile / p.tiles_x) * TY;
+    const int xe = p.o0[3] + p.on[3], ye = p.o0[2] + p.on[2];
+    const int zo_begin = p.o0[1] + seg * p.zseg;
+    const int zo_end = min(zo_begin + p.zseg, p.o0[1] + p.on[1]);
+    const int ot0 = p.o0[0], ot1 = p.o0[0] + p.on[0];
+
+    // ---- S1 points: (ey, ex) of the stage-1 apron, the same for every timepoint ----------
+    int off[NPT];  // byte offset in the plane, or kBad outside the block / past the apron
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+        const int e = tid + k * NT;
+        const int ey = e / E2X, ex = e - (e / E2X) * E2X;
+        const int gy = y0 - 2 * R + ey, gx = x0 - 2 * R + ex;
+        off[k] = (e < C::NE2 && gy >= 0 && gy < ny && gx >= 0 && gx < nx) ? (gy * nx + gx) * 4 : kBad;
+    }
+    const uint32_t plane_bytes = (uint32_t)(plane * 4);
+    auto ldv = [&](int t, int z, int o) -> float {  // v(t, z) at byte offset o; 0 outside
+        const bool in = t < T && (unsigned)z < (unsigned)nz;  // wave-uniform
+        return ldb(make_rsrc(p.v + (in ? t * vol + (int64_t)z * plane : 0), in ? plane_bytes : 0u), o);
+    };
+    const int zc_begin = zo_begin - R, zc_end = zo_end + R;  // stage-1 slices of this march
+    double zv[TS][NPT];
+    float pa[TS][NPT], ps[TS][NPT];
+#pragma unroll
+    for (int t = 0; t < TS; ++t)
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) {
+            double s = 0.0;
+            for (int z = zc_begin - 1 - R; z <= zc_begin - 1 + R; ++z) s += (double)ldv(t, z, off[k]);
+            zv[t][k] = s;
+            pa[t][k] = ldv(t, zc_begin + R, off[k]);
+            ps[t][k] = ldv(t, zc_begin - R - 1, off[k]);
+        }
+
+    // ---- S3 item: column ex1 of the (a, b) apron, rows [KY3*sg, KY3*sg + KY3) --------------
+    const int i3 = tid < C::NI3 ? tid : -1;
+    const int ex3 = i3 % E1X, sg3 = i3 / E1X;
+    const int gx3 = x0 - R + ex3;
+    int off3[C::KY3];
+#pragma unroll
+    for (int j = 0; j < C::KY3; ++j) {
+        const int ey = sg3 * C::KY3 + j, gy = y0 - R + ey;
+        off3[j] = (i3 >= 0 && ey < E1Y && gy >= 0 && gy < ny && gx3 >= 0 && gx3 < nx) ? (gy * nx + gx3) * 4 : kBad;
+    }
+    float v3[TS][C::KY3];  // v at the S3 points of the current stage-1 slice (prefetched)
+    // ---- S5 item: output (y, x) of the tile ----------------------------------------------
+    const int x5 = tid % TX, y5 = tid / TX;  // tid < TX * TY
+    const int gx5 = x0 + x5, gy5 = y0 + y5;
+    const bool live5 = tid < C::NI5 && gx5 < xe && gy5 < ye;
+    const int off5 = live5 ? (gy5 * nx + gx5) * 4 : kBad;
+    const int cyx5 = live5 ? fcount(gy5, ny, R) * fcount(gx5, nx, R) : 0;
+    float v5[TS];
+    // stage-2 z-window: the sum of the last W slice sums P, kept in LDS (each thread only touches
+    // its own slots, so no barrier), summed in a fixed slot order without subtraction
+    if (tid < C::NI5)
+        for (int sl = 0; sl < W * TS; ++sl) Ring[sl * (TY * TX) + tid] = make_float2(0.0f, 0.0f);
+    auto load_v3 = [&](int zc) {
+#pragma unroll
+        for (int t = 0; t < TS; ++t)
+#pragma unroll
+            for (int j = 0; j < C::KY3; ++j) v3[t][j] = ldv(t, zc, off3[j]);
+    };
+    auto load_v5 = [&](int zo) {
+#pragma unroll
+        for (int t = 0; t < TS; ++t) v5[t] = ldv(t, zo, off5);
+    };
+    load_v5(zc_begin - R);
+
+    // count factors of the t-windows (clamped to the block's T)
+    int ta_[TS], tb_[TS];
+#pragma unroll
+    for (int t = 0; t < TS; ++t) {
+        ta_[t] = max(t - R, 0);
+        tb_[t] = min(t + R, T - 1);
+    }
+
+    const int nsteps = zc_end - zc_begin;
+    for (int i = 0, slot = 0; i < nsteps; ++i, slot = slot + 1 == W ? 0 : slot + 1) {
+        {
+            const int zc = zc_begin + i, zo = zc - R;
+            // S1: z-window update, Z1 writes, next step's entering / leaving slices
+#pragma unroll
+            for (int t = 0; t < TS; ++t)
+#pragma unroll
+                for (int k = 0; k < NPT; ++k) {
+                    zv[t][k] = zv[t][k] + (double)pa[t][k];
+                    zv[t][k] = zv[t][k] - (double)ps[t][k];
+                    const int e = tid + k * NT;
+                    if (e < C::NE2) Z1[(t * E2Y + e / E2X) * PZ + e % E2X] = zv[t][k];
+                }
+#pragma unroll
+            for (int t = 0; t < TS; ++t)
+#pragma unroll
+                for (int k = 0; k < NPT; ++k) {
+                    pa[t][k] = ldv(t, zc + 1 + R, off[k]);
+                    ps[t][k] = ldv(t, zc - R, off[k]);
+                }
+            lds_barrier();
+            // S2: x-window sums of every apron row (f64)
+            for (int it = tid; it < C::NI2; it += NT) {
+                const int sx = (it % C::NSX2) * C::KX2, row = it / C::NSX2;  // row = t*E2Y + ey
+                const double* src = Z1 + row * PZ + sx;
+                double in[C::KX2 + 2 * R];
+#pragma unroll
+                for (int j = 0; j < C::KX2 + 2 * R; ++j) in[j] = src[j];
+                double s = 0.0;
+#pragma unroll
+                for (int j = 0; j <= 2 * R; ++j) s += in[j];
+                double* dst = X1 + row * E1X + sx;
+#pragma unroll
+                for (int j = 0; j < C::KX2; ++j) {
+                    if (j > 0) s = s + in[j + 2 * R] - in[j - 1];
+                    if (sx + j < E1X) dst[j] = s;
+                }
+            }
+            lds_barrier();
+            // S3: y-window sums, t-window sums, pointwise stage -> Lab
+            if (i3 >= 0) {
+                load_v3(zc);  // L2 hits: the slice entered stage 1 R steps ago
+                double U3[TS][C::KY3];
+#pragma unroll
+                for (int t = 0; t < TS; ++t) {
+                    const double* src = X1 + (t * E2Y + sg3 * C::KY3) * E1X + ex3;
+                    double in[C::KY3 + 2 * R];
+#pragma unroll
+                    for (int j = 0; j < C::KY3 + 2 * R; ++j) in[j] = src[j * E1X];
+                    double s = 0.0;
+#pragma unroll
+                    for (int j = 0; j <= 2 * R; ++j) s += in[j];
+                    U3[t][0] = s;
+#pragma unroll
+                    for (int j = 1; j < C::KY3; ++j) {
+                        s = s + in[j + 2 * R] - in[j - 1];
+                        U3[t][j] = s;
+                    }
+                }
+                const bool zin = (unsigned)zc < (unsigned)nz;
+                const int czx = zin && gx3 >= 0 && gx3 < nx ? fcount(zc, nz, R) * fcount(gx3, nx, R) : 0;
+#pragma unroll
+                for (int j = 0; j < C::KY3; ++j) {
+                    const int ey = sg3 * C::KY3 + j, gy = y0 - R + ey;
+                    const int cz = gy >= 0 && gy < ny ? czx * fcount(gy, ny, R) : 0;
+#pragma unroll
+                    for (int t = 0; t < TS; ++t) {
+                        double U4 = 0.0;
+#pragma unroll
+                        for (int tt = 0; tt < TS; ++tt)
+                            if (tt >= ta_[t] && tt <= tb_[t]) U4 += U3[tt][j];
+                        float2 ab = make_float2(0.0f, 0.0f);
+                        if (cz > 0 && t < T) {
+                            const float cnt = (float)(cz * (tb_[t] - ta_[t] + 1));
+                            const float u = (float)U4 / cnt;  // summed_area_table_mean
+                            const float d = v3[t][j] - u;
+                            const float sq = d * d;  // (v - u).powf(2.0)
+                            const float a = sq / (sq + p.eps);
+                            ab = make_float2(a, (1.0f - a) * u);
+                        }
+                        Lab[(t * E1Y + ey) * E1X + ex3] = ab;
+                    }
+                }
+            }
+            lds_barrier();
+            // S4: x-window sums of (a, b) rows on the tile columns
+            if (tid < C::NI4) {
+                const int sx = (tid % (TX / C::KX4)) * C::KX4, row = tid / (TX / C::KX4);
+                const int t = row / E1Y, ey = row - t * E1Y;
+                const float2* src = Lab + (t * E1Y + ey) * E1X + sx;
+                float2 in[C::KX4 + 2 * R];
+#pragma unroll
+                for (int j = 0; j < C::KX4 + 2 * R; ++j) in[j] = src[j];
+                float sa = 0.0f, sb = 0.0f;
+#pragma unroll
+                for (int j = 0; j <= 2 * R; ++j) {
+                    sa += in[j].x;
+                    sb += in[j].y;
+                }
+                float2* dst = Hab + row * TX + sx;
+                dst[0] = make_float2(sa, sb);
+#pragma unroll
+                for (int j = 1; j < C::KX4; ++j) {
+                    sa = sa + in[j + 2 * R].x - in[j - 1].x;
+                    sb = sb + in[j + 2 * R].y - in[j - 1].y;
+                    dst[j] = make_float2(sa, sb);
+                }
+            }
+            lds_barrier();
+            // S5: y-window and t-window sums -> ring; emit out(zo) once the ring is full
+            if (tid < C::NI5) {
+                float2 P3[TS];
+#pragma unroll
+                for (int t = 0; t < TS; ++t) {
+                    const float2* src = Hab + (t * E1Y + y5) * TX + x5;
+                    float sa = 0.0f, sb = 0.0f;
+#pragma unroll
+                    for (int j = 0; j <= 2 * R; ++j) {
+                        const float2 q = src[j * TX];
+                        sa += q.x;
+                        sb += q.y;
+                    }
+                    P3[t] = make_float2(sa, sb);
+                }
+#pragma unroll
+                for (int t = 0; t < TS; ++t) {
+                    float sa = 0.0f, sb = 0.0f;
+#pragma unroll
+                    for (int tt = 0; tt < TS; ++tt)
+                        if (tt >= ta_[t] && tt <= tb_[t]) {
+                            sa += P3[tt].x;
+                            sb += P3[tt].y;
+                        }
+                    Ring[(slot * TS + t) * (TY * TX) + tid] = make_float2(sa, sb);
+                }
+                if (i >= 2 * R && live5) {
+                    const int cz5 = fcount(zo, nz, R) * cyx5;
+#pragma unroll
+                    for (int t = 0; t < TS; ++t) {
+                        if (t < ot0 || t >= ot1) continue;
+                        float sa = 0.0f, sb = 0.0f;
+#pragma unroll
+                        for (int sl = 0; sl < W; ++sl) {
+                            const float2 q = Ring[(sl * TS + t) * (TY * TX) + tid];
+                            sa += q.x;
+                            sb += q.y;
+                        }
+                        const float cnt = (float)(cz5 * (tb_[t] - ta_[t] + 1));
+                        const float ma = sa / cnt, mb = sb / cnt;
+                        const float o = __fadd_rn(__fmul_rn(v5[t], ma), mb);  // v *= ma; v += mb
+                        static_cast<TOut*>(p.out)[(t - ot0) * p.os[0] +
+                                                  (int64_t)(zo - p.o0[1]) * p.os[1] +
+                                                  (int64_t)(gy5 - p.o0[2]) * p.os[2] +
+                                                  (int64_t)(gx5 - p.o0[3]) * p.os[3]] =
+                            from_f32<TOut>(o);
+                    }
+                }
+            }
+            load_v5(zo + 1);
+            // the next step's Z1 / Lab writes follow this step's S4 reads (third barrier); its X1
+            // writes follow its first barrier, after every S5 read of Hab
+        }
+    }
+}
+
+template <int R, typename TOut>
+hipError_t launch_fused4(G4FParams p, hipStream_t s) {
+    using C = G4FConfig<R>;
+    p.tiles_x = (p.on[3] + C::TX - 1) / C::TX;
+    p.tiles_y = (p.on[2] + C::TY - 1) / C::TY;
+    const int64_t tiles = (int64_t)p.tiles_x * p.tiles_y;
+    // z segments: enough workgroups for about four per CU, at least 32 output slices each
+    // (a segment recomputes 2R stage-1 slices)
+    int64_t nseg = std::max<int64_t>(1, std::min<int64_t>((p.on[1] + 31) / 32, (1024 + tiles - 1) / tiles));
+    p.zseg = (int)((p.on[1] + nseg - 1) / nseg);
+    nseg = (p.on[1] + p.zseg - 1) / p.zseg;
+    const int64_t gx = tiles * nseg;
+    if (gx > 0x7FFFFFFF) return hipErrorInvalidValue;
+    auto kern = g4_fused_kernel<R, TOut>;
+    static bool attr = false;  // > 64 KB of dynamic LDS needs the opt-in
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    hipLaunchKernelGGL(kern, dim3((unsigned)gx), dim3(C::NT), C::LDS, s, p);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+bool guided4d_fused_supports(int radius, const NdGeom& g) {
+    // slices addressed by 32-bit byte offsets
+    return (radius == 1 || radius == 2) && g.ndim == 4 && g.shape[0] <= kFTS &&
+           g.shape[1] <= 0x7FFFFFFF && g.shape[2] * g.shape[3] * 4 <= 0x7FFFFFFF;
+}
+
+hipError_t launch_guided4d_fused(const float* v, void* out, int dtype_out, const NdGeom& g,
+                                 int radius, float eps, hipStream_t s) {
+    if (g.numel <= 0 || g.out_numel <= 0) return hipSuccess;
+    if (!guided4d_fused_supports(radius, g)) return hipErrorInvalidValue;
+    G4FParams p{};
+    p.v = v;
+    p.out = out;
+    p.T = (int)g.shape[0];
+    p.nz = (int)g.shape[1];
+    p.ny = (int)g.shape[2];
+    p.nx = (int)g.shape[3];
+    p.eps = eps;
+    for (int d = 0; d < 4; ++d) {
+        p.o0[d] = (int)g.out_start[d];
+        p.on[d] = (int)g.out_shape[d];
+        p.os[d] = g.out_strides[d];
+    }
+    hipError_t e = hipErrorInvalidValue;
+    if (radius == 1) {
+        ZT_DISPATCH_DTYPE(dtype_out, TO, e = (launch_fused4<1, TO>(p, s)))
+    } else {
+        ZT_DISPATCH_DTYPE(dtype_out, TO, e = (launch_fused4<2, TO>(p, s)))
+    }
+    return e;
+}
+
+}  // namespace zt

@@ -13,6 +13,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+#include <type_traits>
+
 #include "zt_device.hpp"
 #include "zt_kernels.hpp"
 
@@ -306,6 +309,183 @@ hipError_t launch_gaussian_yx(const void* in, int dtype_in, float* out, int64_t 
                            out, outer, py, px);
         err = hipGetLastError())
     return err;
+}
+
+// ---------------------------------------------------------------------------------------------
+// All three passes of a 3-D block in one z-march. A workgroup owns a 32 x 64 output tile of the
+// (y, x) plane and a segment of output slices; each thread keeps, for its points of the staged
+// (32 + L - 1) x (64 + L - 1) input tile (coordinates clamped as the y / x passes clamp), the L
+// input slices of the current z window in registers (a ring whose slot of window position i is
+// a compile-time constant: the march is unrolled by L), the next entering slice prefetched a step
+// ahead. Per output slice: the z pass from the ring into LDS, then the y and x passes of
+// gauss_yx_fast_kernel. Each element's sums are the reference's (sum = sum + x[i] * w[i] from
+// -0.0, i ascending, no FMA), pass by pass in axis order, so the result is bit-identical to the
+// three separate passes, with one read of the input and one write of the output per element.
+// ---------------------------------------------------------------------------------------------
+constexpr int kZYXTy = 32, kZYXTx = 64, kZYXSegMin = 32;
+
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        static_for<B + 1, E>(f);
+    }
+}
+
+template <int L, typename TIn>
+__global__ __launch_bounds__(256) void gauss_zyx_kernel(const TIn* __restrict__ in,
+                                                        float* __restrict__ out, GaussZYX p,
+                                                        int tiles_x, int tiles_y, int zseg) {
+    constexpr int TY = kZYXTy, TX = kZYXTx, TH = TY + L - 1, TW = TX + L - 1, MID = L / 2;
+    constexpr int NE = TH * TW, NPT = (NE + 255) / 256;
+    __shared__ float tile[TH * TW];
+    __shared__ float ybuf[TY * TW];
+    const int tid = threadIdx.x;
+    const int64_t nz = p.n[0], ny = p.n[1], nx = p.n[2];
+    const int64_t onz = p.on[0], ony = p.on[1], onx = p.on[2];
+    // XCD-aware block -> (tile, z segment): consecutive logical ids (x-adjacent tiles of one
+    // segment) share an XCD, so their y / x aprons come from that XCD's L2
+    const int nwg = gridDim.x, b = blockIdx.x;
+    const int lid = (nwg % 8 == 0) ? (b % 8) * (nwg / 8) + b / 8 : b;
+    const int ntiles = tiles_x * tiles_y;
+    const int tile_i = lid % ntiles, seg = lid / ntiles;
+    const int64_t x0 = (int64_t)(tile_i % tiles_x) * TX, y0 = (int64_t)(tile_i / tiles_x) * TY;
+    const int64_t kz0 = (int64_t)seg * zseg, kz1 = kz0 + zseg < onz ? kz0 + zseg : onz;
+    const int hy = (int)(ony - y0 < TY ? ony - y0 : TY);
+    const int hx = (int)(onx - x0 < TX ? onx - x0 : TX);
+    const int64_t qy0 = p.o0[1] + y0 - MID, qx0 = p.o0[2] + x0 - MID;
+    const int64_t plane = ny * nx;
+    int off[NPT];  // plane offset of each owned tile point (clamped, as the y / x passes clamp)
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+        const int e = tid + 256 * k;
+        const int r = e / TW, c = e - r * TW;
+        int64_t qy = qy0 + r, qx = qx0 + c;
+        qy = qy < 0 ? 0 : (qy > ny - 1 ? ny - 1 : qy);
+        qx = qx < 0 ? 0 : (qx > nx - 1 ? nx - 1 : qx);
+        off[k] = e < NE ? (int)(qy * nx + qx) : 0;
+    }
+    for (int64_t o = blockIdx.y; o < p.outer; o += gridDim.y) {
+        const TIn* vol = in + o * nz * plane;
+        auto ld = [&](int64_t zq, float (&v)[NPT]) {  // input slice zq (clamped) at the points
+            zq = zq < 0 ? 0 : (zq > nz - 1 ? nz - 1 : zq);
+            const TIn* sl = vol + zq * plane;
+#pragma unroll
+            for (int k = 0; k < NPT; ++k) v[k] = Elem<TIn>::to_f32(sl[off[k]]);
+        };
+        float ring[L][NPT], pre[NPT];
+        // window of the first output slice: position i = input slice o0 + kz0 + i - MID in slot
+        // i; position L - 1 arrives through pre
+#pragma unroll
+        for (int i = 0; i < L - 1; ++i) ld(p.o0[0] + kz0 + i - MID, ring[i]);
+        ld(p.o0[0] + kz0 + L - 1 - MID, pre);
+        for (int64_t kb = kz0; kb < kz1; kb += L) {
+            static_for<0, L>([&](auto PH_) {
+                constexpr int PH = decltype(PH_)::value;
+                const int64_t kz = kb + PH;
+                if (kz >= kz1) return;  // block-uniform
+                // slot of window position i at this phase: (PH + i) % L; position L - 1 is new
+#pragma unroll
+                for (int k = 0; k < NPT; ++k) ring[(PH + L - 1) % L][k] = pre[k];
+                if (kz + 1 < kz1) ld(p.o0[0] + kz + 1 + MID, pre);  // next step's entering slice
+#pragma unroll
+                for (int k = 0; k < NPT; ++k) {
+                    float sum = -0.0f;  // Iterator::sum::<f32> (kernel.rs:46, :66)
+#pragma unroll
+                    for (int i = 0; i < L; ++i) sum = sum + ring[(PH + i) % L][k] * p.w[0][i];
+                    if (tid + 256 * k < NE) tile[tid + 256 * k] = sum;
+                }
+                __syncthreads();
+                for (int item = tid; item < TW * (TY / 4); item += 256) {  // y pass, 4 rows
+                    const int c = item % TW, r0 = (item / TW) * 4;
+                    float v[4 + L - 1];
+#pragma unroll
+                    for (int j = 0; j < 4 + L - 1; ++j) v[j] = tile[(r0 + j) * TW + c];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        float sum = -0.0f;
+#pragma unroll
+                        for (int i = 0; i < L; ++i) sum = sum + v[k + i] * p.w[1][i];
+                        ybuf[(r0 + k) * TW + c] = sum;
+                    }
+                }
+                __syncthreads();
+                for (int item = tid; item < TY * (TX / 4); item += 256) {  // x pass, 4 columns
+                    const int r = item / (TX / 4), c0 = (item % (TX / 4)) * 4;
+                    if (r >= hy || c0 >= hx) continue;
+                    float v[4 + L - 1];
+#pragma unroll
+                    for (int j = 0; j < 4 + L - 1; ++j) v[j] = ybuf[r * TW + c0 + j];
+                    float o4[4];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        float sum = -0.0f;
+#pragma unroll
+                        for (int i = 0; i < L; ++i) sum = sum + v[k + i] * p.w[2][i];
+                        o4[k] = sum;
+                    }
+                    float* dst = out + ((o * onz + kz) * ony + y0 + r) * onx + x0 + c0;
+                    if (c0 + 4 <= hx && ((uintptr_t)dst & 15) == 0) {
+                        typedef float v4f __attribute__((ext_vector_type(4)));
+                        const v4f q = {o4[0], o4[1], o4[2], o4[3]};
+                        __builtin_nontemporal_store(q, reinterpret_cast<v4f*>(dst));
+                    } else {
+#pragma unroll
+                        for (int k = 0; k < 4; ++k)
+                            if (c0 + k < hx) dst[k] = o4[k];
+                    }
+                }
+                // the next tile / ybuf writes follow this step's barriers (see gauss_yx_fast)
+            });
+        }
+        __syncthreads();  // the last step's reads of tile / ybuf before the next outer volume
+    }
+}
+
+bool gaussian_zyx_supported(const GaussZYX& p, int dtype_in) {
+    (void)dtype_in;
+    return p.len >= 3 && p.len <= kGaussZYXMaxLen && p.len % 2 == 1 &&
+           p.n[1] * p.n[2] < 0x7FFFFFFF && (p.on[1] + kZYXTy - 1) / kZYXTy <= 0xFFFF &&
+           (p.on[2] + kZYXTx - 1) / kZYXTx <= 0xFFFF;
+}
+
+template <int L>
+static hipError_t launch_zyx_l(const void* in, int dtype_in, float* out, const GaussZYX& p,
+                               hipStream_t s) {
+    const int tiles_x = (int)((p.on[2] + kZYXTx - 1) / kZYXTx);
+    const int tiles_y = (int)((p.on[1] + kZYXTy - 1) / kZYXTy);
+    const int64_t tiles = (int64_t)tiles_x * tiles_y;
+    const int64_t outer = p.outer;
+    // z segments: about 4 workgroups per CU over the whole launch, at least kZYXSegMin slices
+    // each (a segment re-reads L - 1 slices to fill its window)
+    const int64_t want = (2048 + tiles * outer - 1) / (tiles * outer);
+    int64_t nseg = std::max<int64_t>(1, std::min<int64_t>(want, (p.on[0] + kZYXSegMin - 1) / kZYXSegMin));
+    const int zseg = (int)((p.on[0] + nseg - 1) / nseg);
+    nseg = (p.on[0] + zseg - 1) / zseg;
+    const int64_t gx = tiles * nseg;
+    if (gx > 0x7FFFFFFF) return hipErrorInvalidValue;
+    const dim3 grid((unsigned)gx, (unsigned)(outer < 65535 ? outer : 65535));
+    hipError_t err = hipErrorInvalidValue;
+    ZT_DISPATCH_DTYPE(dtype_in, T,
+        hipLaunchKernelGGL((gauss_zyx_kernel<L, T>), grid, dim3(256), 0, s,
+                           static_cast<const T*>(in), out, p, tiles_x, tiles_y, zseg);
+        err = hipGetLastError())
+    return err;
+}
+
+hipError_t launch_gaussian_zyx(const void* in, int dtype_in, float* out, const GaussZYX& p,
+                               hipStream_t s) {
+    if (p.outer * p.on[0] * p.on[1] * p.on[2] == 0) return hipSuccess;
+    if (!gaussian_zyx_supported(p, dtype_in)) return hipErrorInvalidValue;
+    switch (p.len) {
+    case 3: return launch_zyx_l<3>(in, dtype_in, out, p, s);
+    case 5: return launch_zyx_l<5>(in, dtype_in, out, p, s);
+    case 7: return launch_zyx_l<7>(in, dtype_in, out, p, s);
+    case 9: return launch_zyx_l<9>(in, dtype_in, out, p, s);
+    case 11: return launch_zyx_l<11>(in, dtype_in, out, p, s);
+    case 13: return launch_zyx_l<13>(in, dtype_in, out, p, s);
+    default: return hipErrorInvalidValue;
+    }
 }
 
 static dim3 rows_grid(int64_t gx, int64_t rows) {

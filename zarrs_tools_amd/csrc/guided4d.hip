@@ -156,26 +156,35 @@ __global__ __launch_bounds__(kNT) void box3_march_kernel(const TV* __restrict__ 
 }
 
 // K2: u, s, a, b for every timepoint of a voxel (guided_filter.rs:126-142) with 4-D counts.
+// One thread per x of a (z, y) row (3-D grid: no 64-bit index division); the T values of U3
+// are read once into registers (T <= TMAX at compile time).
+template <int TMAX>
 __global__ __launch_bounds__(256) void g4_pointwise_kernel(const double* __restrict__ U3,
                                                            const float* __restrict__ v,
                                                            float2* __restrict__ AB, int T,
                                                            int nz, int ny, int nx, int r,
                                                            float eps) {
     const int64_t vol = (int64_t)nz * ny * nx;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < vol;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        const int x = (int)(i % nx);
-        const int64_t q = i / nx;
-        const int y = (int)(q % ny), z = (int)(q / ny);
-        const int c3 = ccount(z, nz, r) * ccount(y, ny, r) * ccount(x, nx, r);
-        for (int t = 0; t < T; ++t) {
+    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
+    if (x >= nx) return;
+    const int cyx = ccount(y, ny, r) * ccount(x, nx, r);
+    for (int z = blockIdx.z; z < nz; z += gridDim.z) {
+        const int64_t i = ((int64_t)z * ny + y) * nx + x;
+        const int c3 = ccount(z, nz, r) * cyx;
+        double U[TMAX];
+#pragma unroll
+        for (int t = 0; t < TMAX; ++t) U[t] = t < T ? U3[t * vol + i] : 0.0;
+#pragma unroll
+        for (int t = 0; t < TMAX; ++t) {
+            if (t >= T) continue;
             double U4 = 0.0;
             const int ta = max(t - r, 0), tb = min(t + r, T - 1);
-            for (int tt = ta; tt <= tb; ++tt) U4 += U3[tt * vol + i];
+#pragma unroll
+            for (int tt = 0; tt < TMAX; ++tt)
+                if (tt >= ta && tt <= tb) U4 += U[tt];
             const float cnt = (float)(c3 * (tb - ta + 1));
             const float u = (float)U4 / cnt;  // summed_area_table_mean: (sum as f32) / count
-            const float vv = v[t * vol + i];
-            const float d = vv - u;
+            const float d = v[t * vol + i] - u;
             const float s = d * d;  // (v - u).powf(2.0)
             const float a = s / (s + eps);
             const float b = (1.0f - a) * u;
@@ -185,33 +194,38 @@ __global__ __launch_bounds__(256) void g4_pointwise_kernel(const double* __restr
 }
 
 // K4: the output region [o0, o0 + on) of the block: t-window sums of S3, means, v*ma + mb.
-template <typename TOut>
+template <int TMAX, typename TOut>
 __global__ __launch_bounds__(256) void g4_final_kernel(const float2* __restrict__ S3,
                                                        const float* __restrict__ v,
                                                        TOut* __restrict__ out, NdGeom g, int r) {
     const int T = (int)g.shape[0], nz = (int)g.shape[1], ny = (int)g.shape[2],
               nx = (int)g.shape[3];
     const int64_t vol = (int64_t)nz * ny * nx;
-    const int64_t on3 = g.out_shape[1] * g.out_shape[2] * g.out_shape[3];
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < on3;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        const int ox = (int)(i % g.out_shape[3]);
-        const int64_t q = i / g.out_shape[3];
-        const int oy = (int)(q % g.out_shape[2]), oz = (int)(q / g.out_shape[2]);
-        const int x = ox + (int)g.out_start[3], y = oy + (int)g.out_start[2],
-                  z = oz + (int)g.out_start[1];
+    const int ox = blockIdx.x * 256 + threadIdx.x, oy = blockIdx.y;
+    if (ox >= (int)g.out_shape[3]) return;
+    const int x = ox + (int)g.out_start[3], y = oy + (int)g.out_start[2];
+    const int cyx = ccount(y, ny, r) * ccount(x, nx, r);
+    const int t0 = (int)g.out_start[0], ont = (int)g.out_shape[0];
+    for (int oz = blockIdx.z; oz < (int)g.out_shape[1]; oz += gridDim.z) {
+        const int z = oz + (int)g.out_start[1];
         const int64_t bi = ((int64_t)z * ny + y) * nx + x;
-        const int c3 = ccount(z, nz, r) * ccount(y, ny, r) * ccount(x, nx, r);
+        const int c3 = ccount(z, nz, r) * cyx;
         const int64_t dbase = oz * g.out_strides[1] + oy * g.out_strides[2] + ox * g.out_strides[3];
-        for (int ot = 0; ot < (int)g.out_shape[0]; ++ot) {
-            const int t = ot + (int)g.out_start[0];
+        float2 S[TMAX];
+#pragma unroll
+        for (int t = 0; t < TMAX; ++t) S[t] = t < T ? S3[t * vol + bi] : make_float2(0.f, 0.f);
+#pragma unroll
+        for (int ot = 0; ot < TMAX; ++ot) {
+            if (ot >= ont) continue;
+            const int t = ot + t0;
             const int ta = max(t - r, 0), tb = min(t + r, T - 1);
             double sa = 0.0, sb = 0.0;
-            for (int tt = ta; tt <= tb; ++tt) {
-                const float2 p = S3[tt * vol + bi];
-                sa += (double)p.x;
-                sb += (double)p.y;
-            }
+#pragma unroll
+            for (int tt = 0; tt < TMAX; ++tt)
+                if (tt >= ta && tt <= tb) {
+                    sa += (double)S[tt].x;
+                    sb += (double)S[tt].y;
+                }
             const float cnt = (float)(c3 * (tb - ta + 1));
             const float ma = (float)sa / cnt, mb = (float)sb / cnt;
             const float o = __fadd_rn(__fmul_rn(v[t * vol + bi], ma), mb);  // v *= ma; v += mb
@@ -251,7 +265,8 @@ hipError_t launch_box3_r(int r, const TV* in, TO* out, int T, int nz, int ny, in
 
 }  // namespace
 
-// radius <= 6: the f64-pair LDS tiles of K3 stay within 64 KB
+// radius <= 6: the f64-pair LDS tiles of K3 stay within 64 KB; T <= 16 and ny <= 65535 are
+// checked by the caller (K2 / K4 hold a voxel's timepoints in registers, y is grid.y)
 bool guided4d_supports(int radius) { return radius >= 1 && radius <= 6; }
 
 int64_t guided4d_scratch_bytes(int64_t numel, bool gather) {
@@ -291,21 +306,36 @@ hipError_t launch_guided4d(const void* in, int dtype_in, void* out, int dtype_ou
     }
     e = launch_box3_r<float, double, double>(radius, v, U3, T, nz, ny, nx, s);
     if (e != hipSuccess) return e;
-    const int64_t vol = (int64_t)nz * ny * nx;
-    const unsigned blocks = (unsigned)std::min<int64_t>((vol + 255) / 256, 256 * 64);
-    hipLaunchKernelGGL(g4_pointwise_kernel, dim3(blocks), dim3(256), 0, s, U3, v, AB, T, nz, ny,
-                       nx, radius, eps);
+    if (ny > 65535 || g.out_shape[2] > 65535) return hipErrorInvalidValue;  // grid.y
+    const dim3 pgrid((unsigned)((nx + 255) / 256), (unsigned)ny,
+                     (unsigned)std::min<int64_t>(nz, std::max<int64_t>(1, 65536 / ((int64_t)ny * ((nx + 255) / 256)) + 1)));
+    if (T <= 4)
+        hipLaunchKernelGGL(g4_pointwise_kernel<4>, pgrid, dim3(256), 0, s, U3, v, AB, T, nz, ny,
+                           nx, radius, eps);
+    else if (T <= 16)
+        hipLaunchKernelGGL(g4_pointwise_kernel<16>, pgrid, dim3(256), 0, s, U3, v, AB, T, nz,
+                           ny, nx, radius, eps);
+    else
+        return hipErrorInvalidValue;
     if ((e = hipGetLastError()) != hipSuccess) return e;
     float2* S3 = reinterpret_cast<float2*>(U3);
     e = launch_box3_r<float2, dd2, float2>(radius, AB, S3, T, nz, ny, nx, s);
     if (e != hipSuccess) return e;
-    const int64_t on3 = g.out_shape[1] * g.out_shape[2] * g.out_shape[3];
-    const unsigned oblocks = (unsigned)std::min<int64_t>((on3 + 255) / 256, 256 * 64);
+    const int64_t onx = g.out_shape[3], ony = g.out_shape[2], onz = g.out_shape[1];
+    const dim3 fgrid((unsigned)((onx + 255) / 256), (unsigned)ony,
+                     (unsigned)std::min<int64_t>(onz, std::max<int64_t>(1, 65536 / (ony * ((onx + 255) / 256)) + 1)));
     e = hipErrorInvalidValue;
-    ZT_DISPATCH_DTYPE(dtype_out, TO,
-        hipLaunchKernelGGL(g4_final_kernel<TO>, dim3(oblocks), dim3(256), 0, s, S3, v,
-                           static_cast<TO*>(out), g, radius);
-        e = hipGetLastError())
+    if (T <= 4) {
+        ZT_DISPATCH_DTYPE(dtype_out, TO,
+            hipLaunchKernelGGL((g4_final_kernel<4, TO>), fgrid, dim3(256), 0, s, S3, v,
+                               static_cast<TO*>(out), g, radius);
+            e = hipGetLastError())
+    } else {
+        ZT_DISPATCH_DTYPE(dtype_out, TO,
+            hipLaunchKernelGGL((g4_final_kernel<16, TO>), fgrid, dim3(256), 0, s, S3, v,
+                               static_cast<TO*>(out), g, radius);
+            e = hipGetLastError())
+    }
     return e;
 }
 

@@ -277,10 +277,11 @@ int run_separable(zt_ctx* ctx, int dtype_in, const void* in, const int64_t* shap
     return ZT_OK;
 }
 
-// 4-D blocks (config T): the four-kernel path of guided4d.hip when the radius fits it and x is
-// the unit-stride axis; the scratch holds U3/S3, AB and (for other element types or strides) f32 v.
-bool use_guided4d(int ndim, int radius, const int64_t* in_strides) {
-    return ndim == 4 && zt::guided4d_supports(radius) && in_strides[3] == 1;
+// 4-D blocks (config T): guided4d.hip when the radius fits it and x is the unit-stride axis;
+// the scratch holds U3/S3, AB and (for other element types or strides) f32 v.
+bool use_guided4d(int ndim, int radius, const int64_t* in_strides, const int64_t* shape) {
+    return ndim == 4 && zt::guided4d_supports(radius) && in_strides[3] == 1 && shape[0] <= 16 &&
+           shape[1] <= 0x7FFFFFFF && shape[2] <= 65535 && shape[3] <= 0x7FFFFFFF;
 }
 
 int run_guided4d(zt_ctx* ctx, int dtype_in, const void* in, const int64_t* shape,
@@ -299,6 +300,39 @@ int run_guided4d(zt_ctx* ctx, int dtype_in, const void* in, const int64_t* shape
         if (shape[d] > INT32_MAX) return fail(ZT_ERR_INVALID_PARAMETERS, "extent exceeds 2^31-1");
     }
     if (g.numel == 0 || g.out_numel == 0) return ZT_OK;
+    // T <= 4, r <= 2: the one-march kernel (g4_fused.hip); ZT_G4_FUSED=0 forces the four-kernel
+    // path (A/B runs and tests)
+    static const bool fused_off = [] {
+        const char* e = getenv("ZT_G4_FUSED");
+        return e && e[0] == '0';
+    }();
+    if (!fused_off && zt::guided4d_fused_supports(radius, g)) {
+        bool contiguous = dtype_in == zt::kF32;
+        int64_t st = 1;
+        for (int d = 3; d >= 0; --d) {
+            if (in_strides[d] != st) contiguous = false;
+            st *= shape[d];
+        }
+        const float* v = static_cast<const float*>(in);
+        if (!contiguous) {  // f32 C-order copy of the block in scratch
+            if (int rc = ctx->ensure_scratch(sizeof(float) * (size_t)g.numel)) return rc;
+            float* vv = static_cast<float*>(ctx->scratch);
+            const size_t esz = zt::dtype_size(dtype_in);
+            for (int64_t t = 0; t < shape[0]; ++t) {
+                hipError_t e = zt::launch_cast_to_f32_3d(
+                    static_cast<const char*>(in) + esz * t * in_strides[0], dtype_in, in_strides[1],
+                    in_strides[2], vv + t * shape[1] * shape[2] * shape[3], shape[1], shape[2],
+                    shape[3], ctx->cur);
+                if (e != hipSuccess) return hip_fail(e, "guided filter 4-D input cast");
+            }
+            v = vv;
+        }
+        if (ctx->timed) ZT_HIP(hipEventRecord(ctx->ev0, ctx->cur));
+        hipError_t e = zt::launch_guided4d_fused(v, out, dtype_out, g, radius, eps, ctx->cur);
+        if (e != hipSuccess) return hip_fail(e, "guided filter 4-D fused launch");
+        if (ctx->timed) ZT_HIP(hipEventRecord(ctx->ev1, ctx->cur));
+        return ZT_OK;
+    }
     if (int rc = ctx->ensure_scratch((size_t)zt::guided4d_scratch_bytes(g.numel, true))) return rc;
     if (ctx->timed) ZT_HIP(hipEventRecord(ctx->ev0, ctx->cur));
     hipError_t e = zt::launch_guided4d(in, dtype_in, out, dtype_out, g, radius, eps,
@@ -511,7 +545,7 @@ int zt_guided_filter_apply_ndarray(zt_ctx* ctx, int dtype_in, const void* in,
             return run_fused3(ctx, dtype_in, in, dom, 0, dom[0], isz, isy, ost, osh, dtype_out,
                               out, osz, osy, epsilon, radius, 0);
     }
-    if (use_guided4d(ndim, radius, is))
+    if (use_guided4d(ndim, radius, is, in_shape))
         return run_guided4d(ctx, dtype_in, in, in_shape, is, out_start, out_shape, dtype_out, out,
                             os, epsilon, radius);
     return run_separable(ctx, dtype_in, in, in_shape, is, ndim, out_start, out_shape, dtype_out,
@@ -583,7 +617,7 @@ int zt_guided_filter_apply_array(zt_ctx* ctx, int dtype_in, const void* in, int 
         int rc = zt_subset_overlap(shape, ndim, ostart, oshape, ov, is0, ish, dst);
         if (rc) return rc;
         size_t free_b = 0, total_b = 0;
-        const bool g4 = use_guided4d(ndim, radius, strides);
+        const bool g4 = use_guided4d(ndim, radius, strides, ish);
         const size_t need =
             g4 ? (size_t)zt::guided4d_scratch_bytes(numel(ish, ndim), true)
                : sizeof(float) * (size_t)zt::separable_scratch_floats(numel(ish, ndim));
@@ -626,7 +660,7 @@ int zt_guided_filter_apply_array(zt_ctx* ctx, int dtype_in, const void* in, int 
             ioff += is0[d] * strides[d];
             ooff += cs[d] * strides[d];
         }
-        rc = use_guided4d(ndim, radius, strides)
+        rc = use_guided4d(ndim, radius, strides, ish)
                  ? run_guided4d(ctx, dtype_in, static_cast<const char*>(in) + esz_in * ioff, ish,
                                 strides, dst, csh, dtype_out,
                                 static_cast<char*>(out) + esz_out * ooff, strides, epsilon,
@@ -737,6 +771,55 @@ int run_gaussian(zt_ctx* ctx, int dtype_in, const void* in, const int64_t* in_sh
     const void* src = in;
     int sdt = dtype_in;
     if (ctx->timed) ZT_HIP(hipEventRecord(ctx->ev0, ctx->cur));
+    // the last three axes in one z-march when they share one tap vector length that fits it
+    if (ndim >= 3) {
+        zt::GaussZYX pz{};
+        pz.outer = numel(in_shape, ndim - 3);
+        float w[zt::kGaussMaxTaps];
+        bool same = true;
+        for (int a = 0; a < 3; ++a) {
+            const int d = ndim - 3 + a;
+            const int64_t len = gaussian_taps(sigma[d], half[d], w);
+            if (a == 0) pz.len = (int)len;
+            if (len != pz.len || len > zt::kGaussZYXMaxLen) {
+                same = false;
+                break;
+            }
+            std::copy(w, w + len, pz.w[a]);
+            pz.n[a] = in_shape[d];
+            pz.on[a] = out_shape[d];
+            pz.o0[a] = out_start[d];
+        }
+        if (same && zt::gaussian_zyx_supported(pz, dtype_in)) {
+            // earlier axes (ndim > 3) first, pass by pass, then the fused three
+            for (int d = 0; d < ndim - 3; ++d) {
+                zt::GaussPass p{};
+                p.outer = numel(cur, d);
+                p.n = cur[d];
+                p.on = out_shape[d];
+                p.o0 = out_start[d];
+                p.inner = numel(cur + d + 1, ndim - d - 1);
+                p.len = (int)gaussian_taps(sigma[d], half[d], p.w);
+                p.mid = p.len / 2;
+                float* dst = bufs[d & 1];
+                hipError_t e = zt::launch_gaussian_pass(src, sdt, dst, p, ctx->cur);
+                if (e != hipSuccess) return hip_fail(e, "gaussian pass launch");
+                src = dst;
+                sdt = zt::kF32;
+                cur[d] = out_shape[d];
+            }
+            pz.outer = numel(cur, ndim - 3);
+            float* dst = !cast_out ? static_cast<float*>(out) : bufs[(ndim - 3) & 1];
+            hipError_t e = zt::launch_gaussian_zyx(src, sdt, dst, pz, ctx->cur);
+            if (e != hipSuccess) return hip_fail(e, "gaussian z/y/x march launch");
+            if (ctx->timed) ZT_HIP(hipEventRecord(ctx->ev1, ctx->cur));
+            if (cast_out) {
+                e = zt::launch_cast_from_f32_3d(dst, dtype_out, out, 0, 0, 1, 1, nout, ctx->cur);
+                if (e != hipSuccess) return hip_fail(e, "gaussian output cast");
+            }
+            return ZT_OK;
+        }
+    }
     // the last two axes in one fused pass when their kernels fit it (and the y extent fits a grid)
     const bool fuse_yx = ndim >= 2 &&
                          gaussian_taps(sigma[ndim - 2], half[ndim - 2], nullptr) <=

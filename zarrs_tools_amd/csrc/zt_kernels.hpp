@@ -71,6 +71,11 @@ hipError_t launch_guided_separable(const void* in, int dtype_in, void* out, int 
 // 4-D guided filter (guided4d.hip): t-window sums of per-timepoint 3-D box sums, four kernels.
 bool guided4d_supports(int radius);
 int64_t guided4d_scratch_bytes(int64_t numel, bool gather);
+// T <= 4 timepoints, r <= 2: both stages of every timepoint in one z-march (g4_fused.hip),
+// f32 C-order input, no scratch.
+bool guided4d_fused_supports(int radius, const NdGeom& g);
+hipError_t launch_guided4d_fused(const float* v, void* out, int dtype_out, const NdGeom& g,
+                                 int radius, float eps, hipStream_t s);
 hipError_t launch_guided4d(const void* in, int dtype_in, void* out, int dtype_out,
                            const NdGeom& g, int radius, float eps, void* scratch, hipStream_t s);
 
@@ -102,6 +107,18 @@ hipError_t launch_gaussian_pass(const void* in, int dtype_in, float* out, const 
 constexpr int kGaussYXMaxLen = 33;
 hipError_t launch_gaussian_yx(const void* in, int dtype_in, float* out, int64_t outer,
                               const GaussPass& py, const GaussPass& px, hipStream_t s);
+
+// The last three axes' passes fused in one z-march (z, y then x; taps L on all three, odd,
+// <= kGaussZYXMaxLen): input outer x nz x ny x nx, f32 output outer x on[0] x on[1] x on[2].
+constexpr int kGaussZYXMaxLen = 13;
+struct GaussZYX {
+    int64_t outer, n[3], on[3], o0[3];
+    int len;
+    float w[3][kGaussZYXMaxLen];
+};
+bool gaussian_zyx_supported(const GaussZYX& p, int dtype_in);
+hipError_t launch_gaussian_zyx(const void* in, int dtype_in, float* out, const GaussZYX& p,
+                               hipStream_t s);
 
 // Synthetic inputs
 hipError_t launch_synth_step_noise_f32(float* out, int64_t n, int64_t plane, int64_t nx_row,
