@@ -19,6 +19,44 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+def cpu_store_baseline(pin, pout, shape, chunk, eps, radius, threads, nchunks):
+    """The reference's CPU path store -> store on a sample of output chunks (GuidedFilter::apply,
+    guided_filter.rs:260-316): per chunk, in a pool of host threads, read the chunk plus its 2r
+    halo from the input store (decode), run the C restatement of apply_ndarray (oracle/, faithful
+    incl. the dead SAT), and write the chunk to the output store (encode). Test infrastructure:
+    the oracle is the baseline here, never the measured product."""
+    import itertools
+    from concurrent.futures import ThreadPoolExecutor
+    import numpy as np
+    from oracle import oracle as O
+    from zarrs_tools_amd import store as S
+    S.create_output_like(pin, pout)
+    grid = [-(-n // c) for n, c in zip(shape, chunk)]
+    coords = list(itertools.islice(itertools.product(*[range(g) for g in grid]), nchunks))
+    h = 2 * radius
+
+    def one(cc):
+        o0 = [c * k for c, k in zip(cc, chunk)]
+        on = [min(k, n - s) for k, n, s in zip(chunk, shape, o0)]
+        i0 = [max(0, s - h) for s in o0]
+        i1 = [min(n, s + e + h) for s, e, n in zip(o0, on, shape)]
+        block = S.read_array(pin, i0, [b - a for a, b in zip(i0, i1)], nthreads=1)
+        out = O.guided_filter_apply_ndarray(block, eps, radius, faithful=True)
+        sub = tuple(slice(s - a, s - a + e) for s, a, e in zip(o0, i0, on))
+        S.write_array(pout, np.ascontiguousarray(out[sub]), o0, nthreads=1)
+        return int(np.prod(on))
+
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:
+        vox = sum(ex.map(one, coords))
+    secs = time.perf_counter() - t0
+    return {"value": round(vox * 4 / 2 ** 30 / secs, 4), "unit": "GiB/s", "cores": threads,
+            "kind": "port", "secs": round(secs, 2),
+            "sample": f"{len(coords)} output chunks of {'x'.join(map(str, chunk))} (first in C "
+                      f"order), store read of chunk + 2r halo, oracle apply_ndarray (faithful), "
+                      f"store write; {threads} host threads"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--size", type=int, default=1024)
@@ -37,6 +75,8 @@ def main():
     ap.add_argument("--t", type=int, default=0,
                     help="4-D time series (config T): T timepoints of nz x size x size")
     ap.add_argument("--t-chunk", type=int, default=4, help="chunk extent along t (4-D)")
+    ap.add_argument("--cpu-chunks", type=int, default=0,
+                    help="also time the CPU store -> store baseline on this many output chunks")
     a = ap.parse_args()
 
     from zarrs_tools_amd import store as S
@@ -97,6 +137,10 @@ def main():
             err = float(np.max(np.abs(got.astype(np.float64) - ref) /
                                np.maximum(1.0, np.abs(ref))))
             res["check"] = {"planes": c, "max_rel_err": err, "ok": err <= 1e-5}
+        if a.cpu_chunks:
+            res["cpu_baseline"] = cpu_store_baseline(pin, os.path.join(work, "cpu.zarr"), shape,
+                                                     chunk, a.eps, a.radius, a.threads,
+                                                     a.cpu_chunks)
         print(json.dumps(res), flush=True)
     finally:
         if not a.keep:

@@ -1,0 +1,58 @@
+#!/usr/bin/env python3
+"""Write pmc_traffic.json (the per-launch HBM traffic bench.py reports as roofline.traffic) from
+the FETCH_SIZE / WRITE_SIZE passes of tools/profile_pmc.sh, keyed to the library build (sha256),
+the workload and the world size, so bench.py only reports it for the build it was measured on.
+
+Usage: make_traffic_json.py PMC_DIR OUT_JSON [size radius]
+Method (MI355X_MICROARCH.md, HBM / rocprofv3): one launch (bench.py --steps 1 --warmup 0), each
+counter in its own run; FETCH_SIZE and WRITE_SIZE are KiB; FETCH_SIZE x2 is the gfx950
+correction for wide (128 B) reads counted as 64 B.
+"""
+import csv
+import glob
+import hashlib
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def total(d, counter, pat="gf3d"):
+    v, n = 0.0, set()
+    for f in glob.glob(os.path.join(d, "*", "run_counter_collection.csv")):
+        for r in csv.DictReader(open(f)):
+            if pat in r["Kernel_Name"] and r["Counter_Name"] == counter:
+                v += float(r["Counter_Value"])
+                n.add(r["Dispatch_Id"])
+    return v, len(n)
+
+
+def main():
+    pmc, out = sys.argv[1], sys.argv[2]
+    size = int(sys.argv[3]) if len(sys.argv) > 3 else 2048
+    radius = int(sys.argv[4]) if len(sys.argv) > 4 else 4
+    fetch, nf = total(os.path.join(pmc, "fetch"), "FETCH_SIZE")
+    write, nw = total(os.path.join(pmc, "write"), "WRITE_SIZE")
+    if nf != 1 or nw != 1:
+        sys.exit(f"expected one launch per pass, got {nf} / {nw}")
+    h = hashlib.sha256()
+    with open(os.path.join(ROOT, "zarrs_tools_amd", "libzarrs_tools_amd.so"), "rb") as f:
+        for blk in iter(lambda: f.read(1 << 20), b""):
+            h.update(blk)
+    vox = size ** 3
+    rd, wr = fetch * 1024 * 2, write * 1024
+    d = {"lib_sha256": h.hexdigest(), "global_shape": [size] * 3, "radius": radius, "world": 1,
+         "kernel": "gf3d_fused_kernel (interior + edge launches of one step)",
+         "hbm_bytes_per_launch": rd + wr, "read_bytes_per_voxel": round(rd / vox, 3),
+         "write_bytes_per_voxel": round(wr / vox, 3),
+         "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate runs of bench.py "
+                   "--steps 1 --warmup 0; FETCH_SIZE x2 (gfx950 wide-read correction), KiB -> "
+                   "bytes; Infinity-Cache hits are counted by these counters"}
+    with open(out, "w") as f:
+        json.dump(d, f, indent=1)
+    print(json.dumps(d))
+
+
+if __name__ == "__main__":
+    main()

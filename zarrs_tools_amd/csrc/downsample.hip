@@ -112,56 +112,6 @@ __global__ __launch_bounds__(256) void downsample_discrete_kernel(const TIn* __r
     }
 }
 
-// 2 x 2 x 2 mean (the pyramid's common case), one thread per 4 consecutive x outputs of one
-// (z, y) row: the 2 x 2 input rows of 8 consecutive elements each come in as one wide load per
-// row when rows are 8-element aligned (VEC), the 4 outputs go out as one store. Per output the
-// f64 sum runs over the window in C order from -0.0, as downsample3_kernel (bit-identical).
-// The grid enumerates (x quad, y, z): no per-element index division.
-template <typename TIn, typename TOut, bool VEC>
-__global__ __launch_bounds__(256) void downsample222_kernel(const TIn* __restrict__ in,
-                                                            TOut* __restrict__ out, int64_t onz,
-                                                            int64_t ony, int64_t onx,
-                                                            int64_t iny, int64_t inx) {
-    const int64_t x0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
-    const int64_t y = blockIdx.y;
-    if (x0 >= onx) return;
-    const int nq = onx - x0 < 4 ? (int)(onx - x0) : 4;
-    for (int64_t z = blockIdx.z; z < onz; z += gridDim.z) {
-        double sum[4] = {-0.0, -0.0, -0.0, -0.0};
-#pragma unroll
-        for (int a = 0; a < 2; ++a)
-#pragma unroll
-            for (int b = 0; b < 2; ++b) {
-                const TIn* row = in + ((2 * z + a) * iny + 2 * y + b) * inx + 2 * x0;
-                TIn v[8];
-                if (VEC && nq == 4) {
-                    constexpr int kBytes = 8 * (int)sizeof(TIn);
-                    constexpr int kAlign = kBytes < 16 ? kBytes : 16;
-                    __builtin_memcpy(v, __builtin_assume_aligned(row, kAlign), kBytes);
-                } else {
-#pragma unroll
-                    for (int e = 0; e < 8; ++e) v[e] = e < 2 * nq ? row[e] : TIn{};
-                }
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    sum[k] += Elem<TIn>::to_f64(v[2 * k]);
-                    sum[k] += Elem<TIn>::to_f64(v[2 * k + 1]);
-                }
-            }
-        TOut o[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) o[k] = from_f64<TOut>(sum[k] / 8.0);
-        TOut* dst = out + (z * ony + y) * onx + x0;
-        if (VEC && nq == 4) {
-            constexpr int kBytes = 4 * (int)sizeof(TOut);
-            constexpr int kAlign = kBytes < 16 ? kBytes : 16;
-            __builtin_memcpy(__builtin_assume_aligned(dst, kAlign), o, kBytes);
-        } else {
-            for (int k = 0; k < nq; ++k) dst[k] = o[k];
-        }
-    }
-}
-
 template <typename TIn, typename TOut>
 static hipError_t launch_ds_types(const void* in, void* out, const DSParams& p, bool discrete,
                                   hipStream_t s) {
@@ -178,25 +128,7 @@ static hipError_t launch_ds_types(const void* in, void* out, const DSParams& p, 
             return hipErrorInvalidValue;
         }
     }
-    if (p.ndim == 3 && p.win[0] == 2 && p.win[1] == 2 && p.win[2] == 2 &&
-        p.out_shape[1] <= 65535) {
-        const int64_t onz = p.out_shape[0], ony = p.out_shape[1], onx = p.out_shape[2];
-        const int64_t gx = (onx + 1023) / 1024;
-        // about 64 K workgroups in all, z looped inside beyond that
-        const int64_t gz = std::max<int64_t>(1, std::min<int64_t>(onz, 65536 / std::max<int64_t>(1, gx * ony) + 1));
-        const dim3 grid((unsigned)gx, (unsigned)ony, (unsigned)std::min<int64_t>(gz, 65535));
-        constexpr size_t kIA = 8 * sizeof(TIn) < 16 ? 8 * sizeof(TIn) : 16;
-        constexpr size_t kOA = 4 * sizeof(TOut) < 16 ? 4 * sizeof(TOut) : 16;
-        const bool vec = p.in_shape[2] % 8 == 0 && onx % 4 == 0 &&
-                         reinterpret_cast<uintptr_t>(in) % kIA == 0 &&
-                         reinterpret_cast<uintptr_t>(out) % kOA == 0;
-        if (vec)
-            hipLaunchKernelGGL((downsample222_kernel<TIn, TOut, true>), grid, dim3(256), 0, s, i, o,
-                               onz, ony, onx, p.in_shape[1], p.in_shape[2]);
-        else
-            hipLaunchKernelGGL((downsample222_kernel<TIn, TOut, false>), grid, dim3(256), 0, s, i,
-                               o, onz, ony, onx, p.in_shape[1], p.in_shape[2]);
-    } else if (p.ndim == 3 && p.win[0] == 2 && p.win[1] == 2 && p.win[2] == 2) {
+    if (p.ndim == 3 && p.win[0] == 2 && p.win[1] == 2 && p.win[2] == 2) {
         hipLaunchKernelGGL((downsample3_kernel<TIn, TOut, 2, 2, 2>), dim3(blocks), dim3(256), 0, s,
                            i, o, p);
     } else {

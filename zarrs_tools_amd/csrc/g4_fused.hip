@@ -11,7 +11,8 @@
 //       + entering slice zc+R, - leaving slice zc-R-1                         -> Z1 (LDS, f64)
 //   S2  x-window sums of Z1 rows on the (64+2R) columns                          -> X1 (LDS, f64)
 //   S3  y-window sums -> U3(t) on the (64+2R) x (8+2R) apron; t-window sums -> U4 (exact);
-//       u = RN(RN_f32(U4) / c4), s = (v-u)^2, a = s/(s+eps), b = (1-a)u;
+//       u = RN(RN_f32(U4) / c4), s = (v-u)^2, a = s/(s+eps), b = (1-a)u (count divisions
+//       correctly rounded through an LDS table of RN(1/c); a within 1 ulp);
 //       zero outside the block (the clamped sums of stage 2)                   -> Lab (LDS, f32 x2)
 //   S4  x-window sums of (a, b) rows on the 64 tile columns                    -> Hab (LDS, f32 x2)
 //   S5  y-window sums + t-window sums of (a, b) -> P(zc), kept in an LDS history of the last
@@ -50,7 +51,9 @@ struct G4FConfig {
     static constexpr int SZ_B = std::max<int>(TS * E2Y * E1X * 8, TS * E1Y * TX * 8);
     static_assert(E1Y % KY3 == 0, "S3 segments tile the apron rows (X1 reads stay in E2Y)");
     static constexpr int SZ_RING = W * TS * TY * TX * 8;  // stage-2 slice history (float2)
-    static constexpr int LDS = SZ_A + SZ_B + SZ_RING;
+    static constexpr int W4 = W * W * W * W;              // largest window count
+    static constexpr int SZ_RCP = ((W4 + 1) * 4 + 15) / 16 * 16;
+    static constexpr int LDS = SZ_A + SZ_B + SZ_RING + SZ_RCP;
     static_assert(NI3 <= NT && NI4 <= NT && NI5 <= NT, "one item per thread in S3-S5");
     static_assert(TX % KX4 == 0, "S4 segments");
     static_assert(LDS <= 160 * 1024, "LDS budget");
@@ -85,6 +88,24 @@ __device__ __forceinline__ float ldb(rsrc_t r, int off) {
     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
 }
 
+// x / d for an integer count d given rcp = RN(1/d): Markstein's correction makes the quotient
+// correctly rounded (= IEEE division) in 3 VALU ops (as gf_fused.hpp's div_by_count).
+__device__ __forceinline__ float div_by_count(float x, float d, float rcp) {
+    const float q = x * rcp;
+    const float r = __builtin_fmaf(-q, d, x);
+    return __builtin_fmaf(r, rcp, q);
+}
+// s / (s + eps): rcp, one Newton step and Markstein's correction (within 1 ulp, almost always
+// correctly rounded; 0/0 gives NaN as in the reference), as gf_fused.hpp's fast_div.
+__device__ __forceinline__ float fast_div(float x, float d) {
+    float y = __builtin_amdgcn_rcpf(d);
+    const float e = __builtin_fmaf(-d, y, 1.0f);
+    y = __builtin_fmaf(e, y, y);
+    const float q = x * y;
+    const float r = __builtin_fmaf(-d, q, x);
+    return __builtin_fmaf(r, y, q);
+}
+
 // Workgroup barrier for the LDS hand-offs only: __syncthreads() also fences global memory, which
 // would drain the loads kept in flight across it (the next slices' prefetches).
 __device__ __forceinline__ void lds_barrier() {
@@ -110,7 +131,14 @@ __global__ __launch_bounds__(G4FConfig<R>::NT) void g4_fused_kernel(G4FParams p)
     double* X1 = reinterpret_cast<double*>(smem + C::SZ_A);        // [TS][E2Y][E1X]
     float2* Hab = reinterpret_cast<float2*>(smem + C::SZ_A);       // [TS][E1Y][TX]
     float2* Ring = reinterpret_cast<float2*>(smem + C::SZ_A + C::SZ_B);  // [W][TS][TY * TX]
+    float* rcp_tab = reinterpret_cast<float*>(smem + C::SZ_A + C::SZ_B + C::SZ_RING);
+    // RN(1/c) of every window count c (Markstein's correction below needs it exactly); published
+    // by the first step's barriers
+    for (int c = threadIdx.x; c <= C::W4; c += NT) rcp_tab[c] = c > 0 ? 1.0f / (float)c : 0.0f;
     const int tid = threadIdx.x;
+    // wave index as a scalar: phases with fewer items than threads branch around whole idle
+    // waves (an exec-masked pass over the code would still cost their issue slots)
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int T = p.T, nz = p.nz, ny = p.ny, nx = p.nx;
     const int64_t plane = (int64_t)ny * nx, vol = (int64_t)nz * plane;
 
@@ -136,10 +164,15 @@ __global__ __launch_bounds__(G4FConfig<R>::NT) void g4_fused_kernel(G4FParams p)
         off[k] = (e < C::NE2 && gy >= 0 && gy < ny && gx >= 0 && gx < nx) ? (gy * nx + gx) * 4 : kBad;
     }
     const uint32_t plane_bytes = (uint32_t)(plane * 4);
-    auto ldv = [&](int t, int z, int o) -> float {  // v(t, z) at byte offset o; 0 outside
+    const char* vbytes = reinterpret_cast<const char*>(p.v);
+    const int64_t vol_bytes = vol * 4, plane_bytes64 = plane * 4;
+    // descriptor of slice z of timepoint t (0 records outside the block: loads read 0); built
+    // once per slice and step, shared by the thread's points
+    auto slice = [&](int t, int z) -> rsrc_t {
         const bool in = t < T && (unsigned)z < (unsigned)nz;  // wave-uniform
-        return ldb(make_rsrc(p.v + (in ? t * vol + (int64_t)z * plane : 0), in ? plane_bytes : 0u), o);
+        return make_rsrc(vbytes + (in ? t * vol_bytes + z * plane_bytes64 : 0), in ? plane_bytes : 0u);
     };
+    auto ldv = [&](int t, int z, int o) -> float { return ldb(slice(t, z), o); };
     const int zc_begin = zo_begin - R, zc_end = zo_end + R;  // stage-1 slices of this march
     double zv[TS][NPT];
     float pa[TS][NPT], ps[TS][NPT];
@@ -178,9 +211,11 @@ __global__ __launch_bounds__(G4FConfig<R>::NT) void g4_fused_kernel(G4FParams p)
         for (int sl = 0; sl < W * TS; ++sl) Ring[sl * (TY * TX) + tid] = make_float2(0.0f, 0.0f);
     auto load_v3 = [&](int zc) {
 #pragma unroll
-        for (int t = 0; t < TS; ++t)
+        for (int t = 0; t < TS; ++t) {
+            const rsrc_t rs = slice(t, zc);
 #pragma unroll
-            for (int j = 0; j < C::KY3; ++j) v3[t][j] = ldv(t, zc, off3[j]);
+            for (int j = 0; j < C::KY3; ++j) v3[t][j] = ldb(rs, off3[j]);
+        }
     };
     auto load_v5 = [&](int zo) {
 #pragma unroll
@@ -211,12 +246,14 @@ __global__ __launch_bounds__(G4FConfig<R>::NT) void g4_fused_kernel(G4FParams p)
                     if (e < C::NE2) Z1[(t * E2Y + e / E2X) * PZ + e % E2X] = zv[t][k];
                 }
 #pragma unroll
-            for (int t = 0; t < TS; ++t)
+            for (int t = 0; t < TS; ++t) {
+                const rsrc_t ra = slice(t, zc + 1 + R), rl = slice(t, zc - R);
 #pragma unroll
                 for (int k = 0; k < NPT; ++k) {
-                    pa[t][k] = ldv(t, zc + 1 + R, off[k]);
-                    ps[t][k] = ldv(t, zc - R, off[k]);
+                    pa[t][k] = ldb(ra, off[k]);
+                    ps[t][k] = ldb(rl, off[k]);
                 }
+            }
             lds_barrier();
             // S2: x-window sums of every apron row (f64)
             for (int it = tid; it < C::NI2; it += NT) {
@@ -237,7 +274,7 @@ __global__ __launch_bounds__(G4FConfig<R>::NT) void g4_fused_kernel(G4FParams p)
             }
             lds_barrier();
             // S3: y-window sums, t-window sums, pointwise stage -> Lab
-            if (i3 >= 0) {
+            if (wave < (C::NI3 + 63) / 64 && i3 >= 0) {
                 load_v3(zc);  // L2 hits: the slice entered stage 1 R steps ago
                 double U3[TS][C::KY3];
 #pragma unroll
@@ -270,11 +307,12 @@ __global__ __launch_bounds__(G4FConfig<R>::NT) void g4_fused_kernel(G4FParams p)
                             if (tt >= ta_[t] && tt <= tb_[t]) U4 += U3[tt][j];
                         float2 ab = make_float2(0.0f, 0.0f);
                         if (cz > 0 && t < T) {
-                            const float cnt = (float)(cz * (tb_[t] - ta_[t] + 1));
-                            const float u = (float)U4 / cnt;  // summed_area_table_mean
+                            const int c = cz * (tb_[t] - ta_[t] + 1);
+                            // summed_area_table_mean: (sum as f32) / count, correctly rounded
+                            const float u = div_by_count((float)U4, (float)c, rcp_tab[c]);
                             const float d = v3[t][j] - u;
                             const float sq = d * d;  // (v - u).powf(2.0)
-                            const float a = sq / (sq + p.eps);
+                            const float a = fast_div(sq, sq + p.eps);
                             ab = make_float2(a, (1.0f - a) * u);
                         }
                         Lab[(t * E1Y + ey) * E1X + ex3] = ab;
@@ -283,7 +321,7 @@ __global__ __launch_bounds__(G4FConfig<R>::NT) void g4_fused_kernel(G4FParams p)
             }
             lds_barrier();
             // S4: x-window sums of (a, b) rows on the tile columns
-            if (tid < C::NI4) {
+            if (wave < (C::NI4 + 63) / 64 && tid < C::NI4) {
                 const int sx = (tid % (TX / C::KX4)) * C::KX4, row = tid / (TX / C::KX4);
                 const int t = row / E1Y, ey = row - t * E1Y;
                 const float2* src = Lab + (t * E1Y + ey) * E1X + sx;
@@ -307,7 +345,7 @@ __global__ __launch_bounds__(G4FConfig<R>::NT) void g4_fused_kernel(G4FParams p)
             }
             lds_barrier();
             // S5: y-window and t-window sums -> ring; emit out(zo) once the ring is full
-            if (tid < C::NI5) {
+            if (wave < (C::NI5 + 63) / 64 && tid < C::NI5) {
                 float2 P3[TS];
 #pragma unroll
                 for (int t = 0; t < TS; ++t) {
@@ -344,8 +382,9 @@ __global__ __launch_bounds__(G4FConfig<R>::NT) void g4_fused_kernel(G4FParams p)
                             sa += q.x;
                             sb += q.y;
                         }
-                        const float cnt = (float)(cz5 * (tb_[t] - ta_[t] + 1));
-                        const float ma = sa / cnt, mb = sb / cnt;
+                        const int c = cz5 * (tb_[t] - ta_[t] + 1);
+                        const float rc = rcp_tab[c], fc = (float)c;
+                        const float ma = div_by_count(sa, fc, rc), mb = div_by_count(sb, fc, rc);
                         const float o = __fadd_rn(__fmul_rn(v5[t], ma), mb);  // v *= ma; v += mb
                         static_cast<TOut*>(p.out)[(t - ot0) * p.os[0] +
                                                   (int64_t)(zo - p.o0[1]) * p.os[1] +

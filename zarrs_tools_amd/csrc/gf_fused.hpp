@@ -51,6 +51,9 @@
 #ifndef GF_LEAVE_AUX
 #define GF_LEAVE_AUX 0  // cache policy of P1's leaving-slice loads
 #endif
+#ifndef GF_WAVE_SKIP
+#define GF_WAVE_SKIP 1  // P4: idle waves branch around the phase
+#endif
 #ifndef GF_NEWTON_A
 #define GF_NEWTON_A 0  // a = s / (s + eps): Markstein's correction on v_rcp_f32 (<= 1 ulp) without
                        // the Newton step on the reciprocal (a enters only f32 window sums)
@@ -928,6 +931,11 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     };
     auto do_p4 = [&](int tid) {  // x-window sums of (a, b) rows -> Hab
         const int item = tid;
+#if GF_WAVE_SKIP
+        // whole waves past the items branch around the phase (scalar test): exec-masked they
+        // would still spend their issue slots on it
+        if (__builtin_amdgcn_readfirstlane(tid >> 6) * 64 >= C::N4) return;
+#endif
         if (item >= C::N4) return;
         if constexpr (ABL & 4096) return;
         const int row = item % C::E1Y, sg = item / C::E1Y;
