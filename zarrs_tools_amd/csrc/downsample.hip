@@ -50,14 +50,16 @@ __global__ __launch_bounds__(256) void downsample_continuous_kernel(const TIn* _
 }
 
 // 3-D fast path (window wz x wy x wx, all compile-time small): C-order f64 sum, same arithmetic.
+// One output per thread; the grid enumerates (x, y, z) so there is no per-output index division
+// (64-bit divisions of indices past 2^32 dominated the 4096^3 pyramid's level 1).
 template <typename TIn, typename TOut, int WZ, int WY, int WX>
 __global__ __launch_bounds__(256) void downsample3_kernel(const TIn* __restrict__ in,
                                                           TOut* __restrict__ out, DSParams p) {
-    const int64_t onx = p.out_shape[2], ony = p.out_shape[1];
+    const int64_t onx = p.out_shape[2], ony = p.out_shape[1], onz = p.out_shape[0];
     const int64_t inx = p.in_shape[2], iny = p.in_shape[1];
-    for (int64_t o = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; o < p.out_numel;
-         o += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t x = o % onx, t = o / onx, y = t % ony, z = t / ony;
+    const int64_t x = (int64_t)blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
+    if (x >= onx) return;
+    for (int64_t z = blockIdx.z; z < onz; z += gridDim.z) {
         const TIn* src = in + ((z * WZ) * iny + y * WY) * inx + x * WX;
         double sum = -0.0;
 #pragma unroll
@@ -67,7 +69,7 @@ __global__ __launch_bounds__(256) void downsample3_kernel(const TIn* __restrict_
 #pragma unroll
                 for (int c = 0; c < WX; ++c)
                     sum += Elem<TIn>::to_f64(src[(a * iny + b) * inx + c]);
-        out[o] = from_f64<TOut>(sum / (double)(WZ * WY * WX));
+        out[(z * ony + y) * onx + x] = from_f64<TOut>(sum / (double)(WZ * WY * WX));
     }
 }
 
@@ -128,9 +130,14 @@ static hipError_t launch_ds_types(const void* in, void* out, const DSParams& p, 
             return hipErrorInvalidValue;
         }
     }
-    if (p.ndim == 3 && p.win[0] == 2 && p.win[1] == 2 && p.win[2] == 2) {
-        hipLaunchKernelGGL((downsample3_kernel<TIn, TOut, 2, 2, 2>), dim3(blocks), dim3(256), 0, s,
-                           i, o, p);
+    if (p.ndim == 3 && p.win[0] == 2 && p.win[1] == 2 && p.win[2] == 2 &&
+        p.out_shape[1] <= 65535) {
+        const int64_t gx = (p.out_shape[2] + 255) / 256, gy = p.out_shape[1];
+        // about 256 K workgroups, z looped inside beyond that
+        const int64_t gz = std::max<int64_t>(
+            1, std::min<int64_t>({p.out_shape[0], (int64_t)65535, 262144 / std::max<int64_t>(1, gx * gy)}));
+        hipLaunchKernelGGL((downsample3_kernel<TIn, TOut, 2, 2, 2>),
+                           dim3((unsigned)gx, (unsigned)gy, (unsigned)gz), dim3(256), 0, s, i, o, p);
     } else {
         hipLaunchKernelGGL((downsample_continuous_kernel<TIn, TOut>), dim3(blocks), dim3(256), 0, s,
                            i, o, p);
