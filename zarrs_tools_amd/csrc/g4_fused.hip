@@ -88,6 +88,10 @@ __device__ __forceinline__ float ldb(rsrc_t r, int off) {
     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
 }
 
+// Packed pair of f32 (v_pk_add_f32 / v_pk_mul_f32 / v_pk_fma_f32: both lanes in one issue).
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+
 // x / d for an integer count d given rcp = RN(1/d): Markstein's correction makes the quotient
 // correctly rounded (= IEEE division) in 3 VALU ops (as gf_fused.hpp's div_by_count).
 __device__ __forceinline__ float div_by_count(float x, float d, float rcp) {
@@ -295,28 +299,42 @@ __global__ __launch_bounds__(G4FConfig<R>::NT) void g4_fused_kernel(G4FParams p)
                 }
                 const bool zin = (unsigned)zc < (unsigned)nz;
                 const int czx = zin && gx3 >= 0 && gx3 < nx ? fcount(zc, nz, R) * fcount(gx3, nx, R) : 0;
+                static_assert(C::KY3 == 2, "the pointwise stage works on the item's row pair");
+                const int ey0 = sg3 * 2, gyp = y0 - R + ey0;
+                const int cz0 = gyp >= 0 && gyp < ny ? czx * fcount(gyp, ny, R) : 0;
+                const int cz1 = gyp + 1 >= 0 && gyp + 1 < ny ? czx * fcount(gyp + 1, ny, R) : 0;
 #pragma unroll
-                for (int j = 0; j < C::KY3; ++j) {
-                    const int ey = sg3 * C::KY3 + j, gy = y0 - R + ey;
-                    const int cz = gy >= 0 && gy < ny ? czx * fcount(gy, ny, R) : 0;
+                for (int t = 0; t < TS; ++t) {
+                    double U0 = 0.0, U1 = 0.0;
 #pragma unroll
-                    for (int t = 0; t < TS; ++t) {
-                        double U4 = 0.0;
-#pragma unroll
-                        for (int tt = 0; tt < TS; ++tt)
-                            if (tt >= ta_[t] && tt <= tb_[t]) U4 += U3[tt][j];
-                        float2 ab = make_float2(0.0f, 0.0f);
-                        if (cz > 0 && t < T) {
-                            const int c = cz * (tb_[t] - ta_[t] + 1);
-                            // summed_area_table_mean: (sum as f32) / count, correctly rounded
-                            const float u = div_by_count((float)U4, (float)c, rcp_tab[c]);
-                            const float d = v3[t][j] - u;
-                            const float sq = d * d;  // (v - u).powf(2.0)
-                            const float a = fast_div(sq, sq + p.eps);
-                            ab = make_float2(a, (1.0f - a) * u);
+                    for (int tt = 0; tt < TS; ++tt)
+                        if (tt >= ta_[t] && tt <= tb_[t]) {
+                            U0 += U3[tt][0];
+                            U1 += U3[tt][1];
                         }
-                        Lab[(t * E1Y + ey) * E1X + ex3] = ab;
-                    }
+                    // the pair of rows in packed f32 (one issue per op for both):
+                    // u = RN(RN_f32(U4) / c) (Markstein with RN(1/c): correctly rounded),
+                    // s = (v-u)^2, a = s/(s+eps), b = (1-a)u   (guided_filter.rs:126-137)
+                    const int nt = tb_[t] - ta_[t] + 1, c0 = cz0 * nt, c1 = cz1 * nt;
+                    const f2 Uf = {(float)U0, (float)U1};
+                    const f2 fc = {(float)c0, (float)c1}, rc = {rcp_tab[c0], rcp_tab[c1]};
+                    f2 q = Uf * rc;
+                    f2 r = pk_fma(-q, fc, Uf);
+                    const f2 u = pk_fma(r, rc, q);
+                    const f2 d = (f2){v3[t][0], v3[t][1]} - u;
+                    const f2 sq = d * d;  // (v - u).powf(2.0)
+                    const f2 den = sq + (f2){p.eps, p.eps};
+                    f2 y = {__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
+                    const f2 e = pk_fma(-den, y, (f2){1.0f, 1.0f});
+                    y = pk_fma(e, y, y);
+                    q = sq * y;
+                    r = pk_fma(-den, q, sq);
+                    const f2 a = pk_fma(r, y, q);
+                    const f2 b = ((f2){1.0f, 1.0f} - a) * u;
+                    const bool ok0 = c0 > 0 && t < T, ok1 = c1 > 0 && t < T;
+                    float2* dst = Lab + (t * E1Y + ey0) * E1X + ex3;
+                    dst[0] = ok0 ? make_float2(a.x, b.x) : make_float2(0.0f, 0.0f);
+                    dst[E1X] = ok1 ? make_float2(a.y, b.y) : make_float2(0.0f, 0.0f);
                 }
             }
             lds_barrier();
@@ -324,68 +342,56 @@ __global__ __launch_bounds__(G4FConfig<R>::NT) void g4_fused_kernel(G4FParams p)
             if (wave < (C::NI4 + 63) / 64 && tid < C::NI4) {
                 const int sx = (tid % (TX / C::KX4)) * C::KX4, row = tid / (TX / C::KX4);
                 const int t = row / E1Y, ey = row - t * E1Y;
-                const float2* src = Lab + (t * E1Y + ey) * E1X + sx;
-                float2 in[C::KX4 + 2 * R];
+                const f2* src = reinterpret_cast<const f2*>(Lab + (t * E1Y + ey) * E1X + sx);
+                f2 in[C::KX4 + 2 * R];
 #pragma unroll
                 for (int j = 0; j < C::KX4 + 2 * R; ++j) in[j] = src[j];
-                float sa = 0.0f, sb = 0.0f;
+                f2 sab = in[0];
 #pragma unroll
-                for (int j = 0; j <= 2 * R; ++j) {
-                    sa += in[j].x;
-                    sb += in[j].y;
-                }
-                float2* dst = Hab + row * TX + sx;
-                dst[0] = make_float2(sa, sb);
+                for (int j = 1; j <= 2 * R; ++j) sab = sab + in[j];
+                f2* dst = reinterpret_cast<f2*>(Hab + row * TX + sx);
+                dst[0] = sab;
 #pragma unroll
                 for (int j = 1; j < C::KX4; ++j) {
-                    sa = sa + in[j + 2 * R].x - in[j - 1].x;
-                    sb = sb + in[j + 2 * R].y - in[j - 1].y;
-                    dst[j] = make_float2(sa, sb);
+                    sab = sab + in[j + 2 * R] - in[j - 1];
+                    dst[j] = sab;
                 }
             }
             lds_barrier();
             // S5: y-window and t-window sums -> ring; emit out(zo) once the ring is full
             if (wave < (C::NI5 + 63) / 64 && tid < C::NI5) {
-                float2 P3[TS];
+                f2 P3[TS];
 #pragma unroll
                 for (int t = 0; t < TS; ++t) {
-                    const float2* src = Hab + (t * E1Y + y5) * TX + x5;
-                    float sa = 0.0f, sb = 0.0f;
+                    const f2* src = reinterpret_cast<const f2*>(Hab + (t * E1Y + y5) * TX + x5);
+                    f2 sab = src[0];
 #pragma unroll
-                    for (int j = 0; j <= 2 * R; ++j) {
-                        const float2 q = src[j * TX];
-                        sa += q.x;
-                        sb += q.y;
-                    }
-                    P3[t] = make_float2(sa, sb);
+                    for (int j = 1; j <= 2 * R; ++j) sab = sab + src[j * TX];
+                    P3[t] = sab;
                 }
+                f2* ring = reinterpret_cast<f2*>(Ring);
 #pragma unroll
                 for (int t = 0; t < TS; ++t) {
-                    float sa = 0.0f, sb = 0.0f;
+                    f2 sab = {0.0f, 0.0f};
 #pragma unroll
                     for (int tt = 0; tt < TS; ++tt)
-                        if (tt >= ta_[t] && tt <= tb_[t]) {
-                            sa += P3[tt].x;
-                            sb += P3[tt].y;
-                        }
-                    Ring[(slot * TS + t) * (TY * TX) + tid] = make_float2(sa, sb);
+                        if (tt >= ta_[t] && tt <= tb_[t]) sab = sab + P3[tt];
+                    ring[(slot * TS + t) * (TY * TX) + tid] = sab;
                 }
                 if (i >= 2 * R && live5) {
                     const int cz5 = fcount(zo, nz, R) * cyx5;
 #pragma unroll
                     for (int t = 0; t < TS; ++t) {
                         if (t < ot0 || t >= ot1) continue;
-                        float sa = 0.0f, sb = 0.0f;
+                        f2 sab = ring[t * (TY * TX) + tid];
 #pragma unroll
-                        for (int sl = 0; sl < W; ++sl) {
-                            const float2 q = Ring[(sl * TS + t) * (TY * TX) + tid];
-                            sa += q.x;
-                            sb += q.y;
-                        }
+                        for (int sl = 1; sl < W; ++sl) sab = sab + ring[(sl * TS + t) * (TY * TX) + tid];
                         const int c = cz5 * (tb_[t] - ta_[t] + 1);
-                        const float rc = rcp_tab[c], fc = (float)c;
-                        const float ma = div_by_count(sa, fc, rc), mb = div_by_count(sb, fc, rc);
-                        const float o = __fadd_rn(__fmul_rn(v5[t], ma), mb);  // v *= ma; v += mb
+                        const f2 rc = {rcp_tab[c], rcp_tab[c]}, fc = {(float)c, (float)c};
+                        // (mean_a, mean_b) = RN(S / c), Markstein (correctly rounded)
+                        const f2 q = sab * rc;
+                        const f2 m = pk_fma(pk_fma(-q, fc, sab), rc, q);
+                        const float o = __fadd_rn(__fmul_rn(v5[t], m.x), m.y);  // v *= ma; v += mb
                         static_cast<TOut*>(p.out)[(t - ot0) * p.os[0] +
                                                   (int64_t)(zo - p.o0[1]) * p.os[1] +
                                                   (int64_t)(gy5 - p.o0[2]) * p.os[2] +
