@@ -64,9 +64,9 @@ const char* zt_last_error(void);
 size_t zt_dtype_size(int dtype);
 /* Number of HIP devices visible (0 on a host without GPUs; never an error). */
 int zt_device_count(int* count);
-/* Fused guided-filter kernel selection (process-wide; for A/B runs and tests, no reference
- * analogue): 0 = default (gf3d_fused_kernel), 1 = the single-barrier kernel (gf_v9.hpp) wherever
- * it applies (radius 1..4, quad-aligned geometry). Returns the previous value. */
+/* Fused guided-filter kernel selection (process-wide, no reference analogue): 0 = the default
+ * gf3d_fused_kernel, the only variant in this library; 1 (the single-barrier kernel, gf_v9.hpp)
+ * is built only by tools/ for A/B timing and is rejected here. Returns the previous value. */
 int zt_set_fused_variant(int variant);
 
 /* One context per (host thread, device): owns a HIP stream, events and reusable scratch. */
