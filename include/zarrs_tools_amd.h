@@ -278,6 +278,13 @@ int zt_store_create_array(const char* path, int dtype, int ndim, const int64_t* 
  * dtype_out (-1 = the input's) and the input fill value cast to it (filter_traits.rs:47-82). */
 int zt_store_create_output_like(const char* in_path, const char* out_path, int dtype_out,
                                 const char* encoding_json);
+/* The output array of a filter step with an explicit output shape (NULL = the input's): what the
+ * store filters create before they run (the downsample output is max(n / stride, 1), so
+ * Downsample::output_shape, downsample.rs:162-168), with the same reencoding. Used to give
+ * device-resident run-config chains (zarrs_filter.rs:338-381) the arrays the store path would
+ * have made, without writing the intermediate data. */
+int zt_store_create_output(const char* in_path, const char* out_path, int dtype_out,
+                           const int64_t* out_shape, int ndim, const char* encoding_json);
 /* Read any subset into a C-order host buffer (missing chunks read as the fill value). */
 int zt_store_read_subset(const char* path, const int64_t* start, const int64_t* shape,
                          void* host_out, int nthreads);

@@ -151,3 +151,24 @@ def test_ome_level_encoding_rule(tmp_path):
                    S.codecs_json(None, shard_inner=(8, 16, 16)))
     assert ZO.level_encoding(S.open_array(tmp_path / "b"), (20, 18, 35)) == {
         "shard_shape": [20, 18, 32], "chunk_shape": [8, 16, 16]}
+
+
+def test_plan_chains_links_only_private_temporaries():
+    from zarrs_tools_amd.zarrs_filter import plan_chains
+    g = {"filter": "guided_filter", "epsilon": 1.0, "radius": 1}
+    # implicit outputs / inputs chain; a named final output ends the chain
+    steps = [dict(g, input="in"), dict(g), dict(g, output="out")]
+    assert plan_chains(steps) == [(0, 2)]
+    # "$t" written by 0 and read only by 1
+    steps = [dict(g, input="in", output="$t"), dict(g, input="$t", output="out")]
+    assert plan_chains(steps) == [(0, 1)]
+    # "$t" read by two steps: no chain through it
+    steps = [dict(g, input="in", output="$t"), dict(g, input="$t", output="o1"),
+             dict(g, input="$t", output="o2")]
+    assert plan_chains(steps) == []
+    # a named (non-temporary) intermediate breaks the chain
+    steps = [dict(g, input="in", output="mid"), dict(g, output="out")]
+    assert plan_chains(steps) == []
+    # two chains separated by a named output
+    steps = [dict(g, input="in"), dict(g, output="m"), dict(g, input="m"), dict(g, output="o")]
+    assert plan_chains(steps) == [(0, 1), (2, 3)]

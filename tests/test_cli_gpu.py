@@ -48,6 +48,67 @@ def test_run_config_chain_guided_then_downsample(tmp_path):
     assert rel_err(got, want) <= FLOAT_TOL
 
 
+def _chain_cfg(tmp_path, inp, final):
+    return [
+        {"filter": "guided_filter", "input": inp, "output": "$gf", "epsilon": 40000.0,
+         "radius": 2, "data_type": "float32"},
+        {"filter": "gaussian", "sigma": [1.0, 1.0, 1.0], "kernel_half_size": [2, 2, 2]},
+        {"filter": "downsample", "output": final, "stride": [2, 2, 2], "data_type": "uint16",
+         "chunk_shape": [8, 8, 8], "bytes_to_bytes_codecs": '[{"name": "gzip", '
+                                                            '"configuration": {"level": 1}}]'},
+    ]
+
+
+def test_device_resident_chain_equals_store_path(tmp_path):
+    """A chain linked by temporaries runs on HBM arrays (zarrs_filter.rs:338-381 run configs,
+    DESIGN.md §7): same output bits and the same output array as the step-by-step store path."""
+    shape, chunk = (40, 44, 48), (16, 16, 16)
+    u = O.synth_u16(shape)
+    S.create_array(tmp_path / "in.zarr", "uint16", shape, chunk)
+    S.write_array(tmp_path / "in.zarr", u)
+    dev_out, store_out = str(tmp_path / "dev.zarr"), str(tmp_path / "store.zarr")
+    logs = []
+    res = ZF.run(_chain_cfg(tmp_path, str(tmp_path / "in.zarr"), dev_out), tmp=str(tmp_path),
+                 log=logs.append)
+    assert len(res) == 3 and all(r.get("device_resident") for r in res), logs
+    res = ZF.run(_chain_cfg(tmp_path, str(tmp_path / "in.zarr"), store_out), tmp=str(tmp_path),
+                 log=logs.append, device_chain=False)
+    assert not any(r.get("device_resident") for r in res)
+    a, b = S.read_array(dev_out), S.read_array(store_out)
+    assert a.dtype == np.uint16 and a.shape == (20, 22, 24)
+    assert np.array_equal(a, b)
+    ma, mb = S.open_array(dev_out).metadata, S.open_array(store_out).metadata
+    assert ma == mb and ma["chunk_grid"]["configuration"]["chunk_shape"] == [8, 8, 8]
+    # the oracle's chain (the guided tolerance carries through the later steps)
+    gf = O.guided_filter_apply(u.astype(np.float32), chunk, 40000.0, 2, nthreads=8)
+    g = O.gaussian_apply(gf, chunk, [1.0] * 3, [2] * 3)
+    want = O.downsample(g, "float32", (2, 2, 2), "float32")
+    assert np.max(np.abs(a.astype(np.float64) - want.astype(np.float64).astype(np.uint16))) <= 1
+    # no temporary survives
+    assert sorted(os.listdir(tmp_path)) == ["dev.zarr", "in.zarr", "store.zarr"]
+
+
+def test_named_temporary_read_twice_is_not_chained(tmp_path):
+    shape, chunk = (24, 20, 36), (8, 8, 16)
+    v = O.synth_step_noise_f32(shape)
+    S.create_array(tmp_path / "in.zarr", "float32", shape, chunk)
+    S.write_array(tmp_path / "in.zarr", v)
+    steps = [
+        {"filter": "guided_filter", "input": str(tmp_path / "in.zarr"), "output": "$a",
+         "epsilon": 2500.0, "radius": 1},
+        {"filter": "downsample", "input": "$a", "output": str(tmp_path / "d1.zarr"),
+         "stride": [2, 2, 2]},
+        {"filter": "gaussian", "input": "$a", "output": str(tmp_path / "g.zarr"),
+         "sigma": [1.0, 1.0, 1.0], "kernel_half_size": [1, 1, 1]},
+    ]
+    assert ZF.plan_chains(steps) == []
+    res = ZF.run(steps, tmp=str(tmp_path), log=lambda *a: None)
+    assert not any(r.get("device_resident") for r in res)
+    gf = O.guided_filter_apply(v, chunk, 2500.0, 1, nthreads=8)
+    assert rel_err(S.read_array(tmp_path / "g.zarr"),
+                   O.gaussian_apply(gf, chunk, [1.0] * 3, [1] * 3)) <= FLOAT_TOL
+
+
 def test_zarrs_ome_levels_and_metadata(tmp_path):
     shape, chunk = (40, 36, 70), (16, 16, 32)
     u = O.synth_u16(shape)

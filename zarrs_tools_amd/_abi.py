@@ -170,6 +170,8 @@ def lib() -> ctypes.CDLL:
                                  i64p, i64p, i64p], c_int),
         "zt_store_create_array": ([ctypes.c_char_p, c_int, c_int, i64p, i64p, ctypes.c_char_p,
                                    ctypes.c_char_p], c_int),
+        "zt_store_create_output": ([ctypes.c_char_p, ctypes.c_char_p, c_int, i64p, c_int,
+                                    ctypes.c_char_p], c_int),
         "zt_store_create_output_like": ([ctypes.c_char_p, ctypes.c_char_p, c_int,
                                          ctypes.c_char_p], c_int),
         "zt_store_set_progress_callback": ([PROGRESS_FN, vp], None),

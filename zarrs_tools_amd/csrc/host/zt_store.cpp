@@ -951,6 +951,29 @@ int zt_store_create_output_like(const char* in_path, const char* out_path, int d
     }
 }
 
+int zt_store_create_output(const char* in_path, const char* out_path, int dtype_out,
+                           const int64_t* out_shape, int ndim, const char* encoding_json) {
+    try {
+        if (!in_path || !out_path) return zt::set_last_error(ZT_ERR_INVALID_PARAMETERS, "null path");
+        Array in = Array::open(in_path);
+        std::vector<int64_t> shape = in.shape;
+        if (out_shape) {
+            if (ndim != in.ndim())
+                return zt::set_last_error(ZT_ERR_INVALID_PARAMETERS, "output rank != input rank");
+            for (int d = 0; d < ndim; ++d) {
+                if (out_shape[d] < 0)
+                    return zt::set_last_error(ZT_ERR_INVALID_PARAMETERS, "negative output extent");
+                shape[d] = out_shape[d];
+            }
+        }
+        Array out = build_output(in, out_path, dtype_out, shape, encoding_json);
+        out.store_metadata();
+        return ZT_OK;
+    } catch (const std::exception& e) {
+        return report(e);
+    }
+}
+
 int zt_store_guided_filter(const char* in_path, const char* out_path, int dtype_out,
                            const char* encoding_json, float epsilon, int radius, int device,
                            int64_t row_begin, int64_t row_end, int nthreads, int flags,

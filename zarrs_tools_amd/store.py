@@ -173,6 +173,16 @@ def create_output_like(input_path, output_path, data_type: Optional[str] = None,
                                             _enc(encoding)))
 
 
+def create_output(input_path, output_path, data_type: Optional[str] = None, shape=None,
+                  encoding=None) -> None:
+    """The output array of a filter step with an explicit shape (None = the input's), as the
+    store filters create it (reencoding included), zarr.json written, no chunk data."""
+    nd = 0 if shape is None else len(shape)
+    check(lib().zt_store_create_output(_b(input_path), _b(output_path), _dt(data_type),
+                                       None if shape is None else i64_array(shape), nd,
+                                       _enc(encoding)))
+
+
 def _flags(erase: bool, finish: bool) -> int:
     return (_abi.STORE_ERASE_OUTPUT_METADATA if erase else 0) | (
         _abi.STORE_FINISH_OUTPUT if finish else 0)

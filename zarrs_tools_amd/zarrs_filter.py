@@ -14,6 +14,11 @@ accelerates:
 * a JSON run config is a list of {"filter": "guided_filter" | "downsample", "input", "output",
   ...args, "data_type"}, with "$name" meaning a named temporary array under --tmp and an omitted
   input meaning the previous filter's output (zarrs_filter.rs:106-138, :338-381);
+* a chain of steps linked only through temporaries (a "$name" or implicit output read by the
+  next step alone) runs device-resident when its arrays fit 80 % of the free device memory: the
+  chain input is read once, every step runs on the arrays in HBM, the last output is written
+  once; the temporaries' zarr.json are created as the store path would create them, but their
+  chunks never go through the store (`--no-device-chain` forces the store path);
 * every filter takes the reencoding arguments (ZarrReencodingArgs, lib.rs:274-377: -d/--data-type,
   -f/--fill-value, --separator, -c/--chunk-shape, -s/--shard-shape, --array-to-array-codecs,
   --array-to-bytes-codec, --bytes-to-bytes-codecs, --dimension-names, --attributes,
@@ -116,6 +121,8 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--chunk-limit", type=int, default=None)
     ap.add_argument("--device", type=int, default=0)
     ap.add_argument("--stats", action="store_true", help="print per-filter stats as JSON")
+    ap.add_argument("--no-device-chain", action="store_true",
+                    help="run every step store -> store, also chains of temporaries")
     sub = ap.add_subparsers(dest="filter")
     g = sub.add_parser("guided-filter", help="Apply a guided filter (edge preserving noise filter).")
     g.add_argument("input")
@@ -154,9 +161,142 @@ def _steps_from_cli(a) -> list:
     return []
 
 
+def _is_temp(p) -> bool:
+    return p is None or (isinstance(p, str) and p.startswith("$"))
+
+
+def plan_chains(steps: list) -> list:
+    """Maximal runs [i, j] of steps (j > i) where every step before j hands its output to the next
+    step only: the output is a temporary (a "$name", or omitted) and the next step reads it (its
+    input is that "$name", or omitted = the previous output), and no other step names it."""
+    refs: dict = {}
+    for st in steps:
+        for key in ("input", "output"):
+            v = st.get(key)
+            if isinstance(v, str) and v.startswith("$"):
+                refs[v] = refs.get(v, 0) + 1
+
+    def linked(k):
+        out, nxt = steps[k].get("output"), steps[k + 1].get("input")
+        if not _is_temp(out):
+            return False
+        if out is None:
+            return nxt is None
+        return nxt in (out, None) and refs.get(out, 0) == (2 if nxt == out else 1)
+
+    chains, i = [], 0
+    while i < len(steps):
+        j = i
+        while j + 1 < len(steps) and linked(j):
+            j += 1
+        if j > i:
+            chains.append((i, j))
+        i = j + 1
+    return chains
+
+
+def _step_params(step, info):
+    """(filter object, output shape, output data type) of a run-config step on an input array."""
+    from . import filter as F
+    name = step.get("filter")
+    dt = step.get("data_type") or (encoding_of(step) or {}).get("data_type") or info.data_type
+    if name == "guided_filter":
+        if "epsilon" not in step or "radius" not in step:
+            raise _abi.InvalidParameters(_abi.ERR_INVALID_PARAMETERS,
+                                         "guided_filter needs epsilon and radius")
+        return F.GuidedFilter(float(step["epsilon"]), int(step["radius"])), tuple(info.shape), dt
+    if name == "gaussian":
+        sigma, half = step.get("sigma"), step.get("kernel_half_size")
+        sigma = _parse_floats(sigma) if isinstance(sigma, str) else sigma
+        half = _parse_stride(half) if isinstance(half, str) else half
+        if not sigma or not half or len(sigma) != info.ndim or len(half) != info.ndim:
+            raise _abi.InvalidParameters(_abi.ERR_INVALID_PARAMETERS,
+                                         "gaussian sigma and kernel_half_size need one entry "
+                                         "per axis")
+        return F.Gaussian(sigma, half), tuple(info.shape), dt
+    stride = step.get("stride")
+    stride = _parse_stride(stride) if isinstance(stride, str) else stride
+    if not stride or len(stride) != info.ndim:
+        raise _abi.InvalidParameters(_abi.ERR_INVALID_PARAMETERS,
+                                     "downsample stride must match the array rank")
+    f = F.Downsample(stride, discrete=bool(step.get("discrete", False)))
+    return f, f.output_shape(info.shape), dt
+
+
+def _nbytes(shape, data_type) -> int:
+    n = 1
+    for s in shape:
+        n *= int(s)
+    return n * S.NUMPY[data_type]().itemsize
+
+
+def run_device_chain(steps: list, paths: list, device: int = 0, nthreads: int = 0,
+                     log=print, budget_frac: float = 0.8):
+    """Run steps[0..] device-resident: paths[k] is step k's input path (paths[k+1] its output).
+    Creates every output array as the store path would (S.create_output), reads paths[0] once,
+    applies the filters on HBM arrays, writes the last output once. Returns per-step stats, or
+    None (nothing done) when the chain's arrays do not fit `budget_frac` of the free device
+    memory, in which case the caller runs it store -> store."""
+    import torch
+    from . import filter as F
+    # shapes / types of every array of the chain (metadata only)
+    plan, info = [], S.open_array(paths[0])
+    peak = 0
+    for k, step in enumerate(steps):
+        f, oshape, odt = _step_params(step, info)
+        peak = max(peak, _nbytes(info.shape, info.data_type) + _nbytes(oshape, odt))
+        plan.append((f, info, oshape, odt))
+        info = S.ArrayInfo(paths[k + 1], odt, tuple(oshape), info.chunk_shape,
+                           info.inner_chunk_shape)
+    free, _total = torch.cuda.mem_get_info(device)
+    if 2 * peak > budget_frac * free:  # in + out of a step, plus filter scratch of the same order
+        return None
+    results = []
+    for k, step in enumerate(steps):
+        f, src_info, oshape, odt = plan[k]
+        S.create_output(paths[k], paths[k + 1], odt, oshape, encoding_of(step))
+    t0 = time.perf_counter()
+    src_info = S.open_array(paths[0])
+    host = S.read_array(paths[0], nthreads=nthreads)
+    t_read = time.perf_counter() - t0
+    dev = torch.device("cuda", device)
+    x = torch.from_numpy(host).to(dev)
+    x_dt, x_chunk = src_info.data_type, src_info.chunk_shape
+    ctx = F.default_context(device)
+    for k, step in enumerate(steps):
+        f = plan[k][0]
+        out_info = S.open_array(paths[k + 1])
+        y = torch.empty(tuple(out_info.shape), dtype=F.torch_dtype(out_info.data_type), device=dev)
+        t1 = time.perf_counter()
+        f.apply(F.DeviceArray(x, x_chunk, x_dt), F.DeviceArray(y, out_info.chunk_shape,
+                                                              out_info.data_type), ctx=ctx)
+        ctx.synchronize()
+        t_k = time.perf_counter() - t1
+        log(f"{k}: {step.get('filter')} device-resident {list(x.shape)} {x_dt} -> "
+            f"{list(y.shape)} {out_info.data_type} in {t_k:.3f}s")
+        results.append({"wall_s": t_k, "decode_s": t_read if k == 0 else 0.0, "encode_s": 0.0,
+                        "h2d_s": 0.0, "kernel_s": t_k, "d2h_s": 0.0, "bytes_read": 0,
+                        "bytes_written": 0, "voxels": int(y.numel()), "rows": 0,
+                        "threads": nthreads, "device_resident": True})
+        x, x_dt, x_chunk = y, out_info.data_type, out_info.chunk_shape
+    t2 = time.perf_counter()
+    out_host = x.cpu().numpy()
+    S.write_array(paths[-1], out_host, nthreads=nthreads)
+    results[-1]["encode_s"] = time.perf_counter() - t2
+    return results
+
+
+def _device_ok(device: int) -> bool:
+    try:
+        import torch
+        return torch.cuda.is_available() and device < torch.cuda.device_count()
+    except Exception:
+        return False
+
+
 def run(steps: list, exists: str = "erase", tmp: str | None = None,
         chunk_limit: int | None = None, device: int = 0, stats: bool = False,
-        log=print) -> list:
+        log=print, device_chain: bool = True) -> list:
     """Run a list of filter steps (the run-config form); returns the per-step stats."""
     tmp_root = tmp or tempfile.gettempdir()
     temps: dict[str, str] = {}
@@ -181,6 +321,68 @@ def run(steps: list, exists: str = "erase", tmp: str | None = None,
             return temps[p]
         return p
 
+    def prepare(dst):
+        if exists == "exit" and os.path.exists(os.path.join(dst, "zarr.json")):
+            raise _abi.FilterError(_abi.ERR_OTHER, f"output {dst} already exists")
+        if os.path.isdir(dst) and dst not in made:
+            # create_array erases the output prefix (zarrs_filter.rs:76); only the
+            # temporaries this run just made (empty) are kept
+            shutil.rmtree(dst)
+
+    def store_step(i, step, src, dst):
+        name = step.get("filter")
+        threads = step.get("chunk_limit") or chunk_limit or 0
+        info = S.open_array(src)
+        if name == "guided_filter":
+            if "epsilon" not in step or "radius" not in step:
+                raise _abi.InvalidParameters(_abi.ERR_INVALID_PARAMETERS,
+                                             "guided_filter needs epsilon and radius")
+            log(f"{i}: guided_filter epsilon={step['epsilon']} radius={step['radius']} "
+                f"{src} ({info.data_type} {list(info.shape)}) -> {dst}")
+            st = S.guided_filter(src, dst, float(step["epsilon"]), int(step["radius"]),
+                                 data_type=step.get("data_type"), device=device,
+                                 nthreads=threads, encoding=encoding_of(step))
+        elif name == "gaussian":
+            sigma, half = step.get("sigma"), step.get("kernel_half_size")
+            if isinstance(sigma, str):
+                sigma = _parse_floats(sigma)
+            if isinstance(half, str):
+                half = _parse_stride(half)
+            if (not sigma or not half or len(sigma) != info.ndim
+                    or len(half) != info.ndim):
+                raise _abi.InvalidParameters(
+                    _abi.ERR_INVALID_PARAMETERS,
+                    "gaussian sigma and kernel_half_size need one entry per axis")
+            log(f"{i}: gaussian sigma={sigma} kernel_half_size={half} "
+                f"{src} ({info.data_type} {list(info.shape)}) -> {dst}")
+            st = S.gaussian(src, dst, sigma, half, data_type=step.get("data_type"),
+                            device=device, nthreads=threads, encoding=encoding_of(step))
+        else:
+            stride = step.get("stride")
+            if isinstance(stride, str):
+                stride = _parse_stride(stride)
+            if not stride or len(stride) != info.ndim:
+                raise _abi.InvalidParameters(_abi.ERR_INVALID_PARAMETERS,
+                                             "downsample stride must match the array rank")
+            log(f"{i}: downsample stride={stride} discrete={bool(step.get('discrete'))} "
+                f"{src} ({info.data_type} {list(info.shape)}) -> {dst}")
+            st = S.downsample(src, dst, stride, discrete=bool(step.get("discrete", False)),
+                              data_type=step.get("data_type"), device=device,
+                              nthreads=threads, encoding=encoding_of(step))
+        out = S.open_array(dst)
+        log(f"   -> {out.data_type} {list(out.shape)} in {st['wall_s']:.2f}s "
+            f"(rw:{st['decode_s']:.2f}/{st['encode_s']:.2f} p:{st['kernel_s']:.3f})")
+        if stats:
+            log(json.dumps({"step": i, "filter": name, **st}))
+        return st
+
+    for step in steps:
+        name = step.get("filter")
+        if name not in ON_PATH:
+            raise _abi.FilterError(_abi.ERR_OTHER,
+                                   f"filter {name!r} is outside the accelerated path "
+                                   f"(supported: {', '.join(ON_PATH)})")
+    chains = dict(plan_chains(steps)) if device_chain and _device_ok(device) else {}
     t_all = time.perf_counter()
     if sys.stderr.isatty():
         def _show(p):
@@ -191,65 +393,27 @@ def run(steps: list, exists: str = "erase", tmp: str | None = None,
             sys.stderr.flush()
         S.set_progress_callback(_show)
     try:
-        for i, step in enumerate(steps):
-            name = step.get("filter")
-            if name not in ON_PATH:
-                raise _abi.FilterError(_abi.ERR_OTHER,
-                                       f"filter {name!r} is outside the accelerated path "
-                                       f"(supported: {', '.join(ON_PATH)})")
-            src = resolve(step.get("input"), "input")
-            dst = resolve(step.get("output"), "output")
-            if exists == "exit" and os.path.exists(os.path.join(dst, "zarr.json")):
-                raise _abi.FilterError(_abi.ERR_OTHER, f"output {dst} already exists")
-            if os.path.isdir(dst) and dst not in made:
-                # create_array erases the output prefix (zarrs_filter.rs:76); only the
-                # temporaries this run just made (empty) are kept
-                shutil.rmtree(dst)
-            threads = step.get("chunk_limit") or chunk_limit or 0
-            info = S.open_array(src)
-            if name == "guided_filter":
-                if "epsilon" not in step or "radius" not in step:
-                    raise _abi.InvalidParameters(_abi.ERR_INVALID_PARAMETERS,
-                                                 "guided_filter needs epsilon and radius")
-                log(f"{i}: guided_filter epsilon={step['epsilon']} radius={step['radius']} "
-                    f"{src} ({info.data_type} {list(info.shape)}) -> {dst}")
-                st = S.guided_filter(src, dst, float(step["epsilon"]), int(step["radius"]),
-                                     data_type=step.get("data_type"), device=device,
-                                     nthreads=threads, encoding=encoding_of(step))
-            elif name == "gaussian":
-                sigma, half = step.get("sigma"), step.get("kernel_half_size")
-                if isinstance(sigma, str):
-                    sigma = _parse_floats(sigma)
-                if isinstance(half, str):
-                    half = _parse_stride(half)
-                if (not sigma or not half or len(sigma) != info.ndim
-                        or len(half) != info.ndim):
-                    raise _abi.InvalidParameters(
-                        _abi.ERR_INVALID_PARAMETERS,
-                        "gaussian sigma and kernel_half_size need one entry per axis")
-                log(f"{i}: gaussian sigma={sigma} kernel_half_size={half} "
-                    f"{src} ({info.data_type} {list(info.shape)}) -> {dst}")
-                st = S.gaussian(src, dst, sigma, half, data_type=step.get("data_type"),
-                                device=device, nthreads=threads, encoding=encoding_of(step))
-            else:
-                stride = step.get("stride")
-                if isinstance(stride, str):
-                    stride = _parse_stride(stride)
-                if not stride or len(stride) != info.ndim:
-                    raise _abi.InvalidParameters(_abi.ERR_INVALID_PARAMETERS,
-                                                 "downsample stride must match the array rank")
-                log(f"{i}: downsample stride={stride} discrete={bool(step.get('discrete'))} "
-                    f"{src} ({info.data_type} {list(info.shape)}) -> {dst}")
-                st = S.downsample(src, dst, stride, discrete=bool(step.get("discrete", False)),
-                                  data_type=step.get("data_type"), device=device,
-                                  nthreads=threads, encoding=encoding_of(step))
-            out = S.open_array(dst)
-            log(f"   -> {out.data_type} {list(out.shape)} in {st['wall_s']:.2f}s "
-                f"(rw:{st['decode_s']:.2f}/{st['encode_s']:.2f} p:{st['kernel_s']:.3f})")
-            if stats:
-                log(json.dumps({"step": i, "filter": name, **st}))
-            results.append(st)
-            last_output = dst
+        i = 0
+        while i < len(steps):
+            j = chains.get(i, i)
+            paths = [resolve(steps[i].get("input"), "input")]
+            for k in range(i, j + 1):
+                d = resolve(steps[k].get("output"), "output")
+                prepare(d)
+                paths.append(d)
+                last_output = d
+            res = None
+            if j > i:
+                threads = chunk_limit or 0
+                res = run_device_chain(steps[i:j + 1], paths, device, threads, log)
+                if res is not None and stats:
+                    for k, st in enumerate(res):
+                        log(json.dumps({"step": i + k, "filter": steps[i + k].get("filter"), **st}))
+            if res is None:  # one step, or a chain too large for the device: store -> store
+                res = [store_step(k, steps[k], paths[k - i], paths[k - i + 1])
+                       for k in range(i, j + 1)]
+            results.extend(res)
+            i = j + 1
     finally:
         if sys.stderr.isatty():
             S.set_progress_callback(None)
@@ -277,7 +441,8 @@ def main(argv=None) -> int:
         build_parser().print_help()
         return 2
     try:
-        run(steps, a.exists, a.tmp, a.chunk_limit, a.device, a.stats)
+        run(steps, a.exists, a.tmp, a.chunk_limit, a.device, a.stats,
+            device_chain=not a.no_device_chain)
     except _abi.FilterError as e:
         print(f"Error: {e}", file=sys.stderr)
         return 1
