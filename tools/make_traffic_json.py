@@ -20,7 +20,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def total(d, counter, pat="gf3d"):
     v, n = 0.0, set()
-    for f in glob.glob(os.path.join(d, "*", "run_counter_collection.csv")):
+    for f in glob.glob(os.path.join(d, "**", "run_counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             if pat in r["Kernel_Name"] and r["Counter_Name"] == counter:
                 v += float(r["Counter_Value"])
