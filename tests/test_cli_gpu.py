@@ -229,3 +229,28 @@ def test_store_single_buffered_under_a_small_memory_budget(tmp_path, monkeypatch
     assert st["double_buffered"] == 0 and st["rows_in_flight"] == 3
     ref = O.guided_filter_apply(O.synth_step_noise_f32(shape), chunk, 2500.0, 2, nthreads=8)
     assert rel_err(S.read_array(tmp_path / "out.zarr"), ref) <= FLOAT_TOL
+
+
+@pytest.mark.parametrize("mode", ["mean", "discrete", "gaussian"])
+def test_zarrs_ome_device_resident_equals_store_levels(tmp_path, mode):
+    """Levels computed from the previous level in HBM equal the reference's loop (each level
+    read back from the store), bit for bit, with the same level metadata."""
+    shape, chunk = (36, 40, 52), (16, 16, 16)
+    u = O.synth_u16(shape)
+    S.create_array(tmp_path / "in.zarr", "uint16", shape, chunk)
+    S.write_array(tmp_path / "in.zarr", u)
+    kw = {"discrete": mode == "discrete"}
+    if mode == "gaussian":
+        kw.update(gaussian_sigma=[1.0, 1.0, 1.0], gaussian_kernel_half_size=[2, 2, 2])
+    a = ZO.run(str(tmp_path / "in.zarr"), str(tmp_path / "dev"), log=lambda *x: None, **kw)
+    b = ZO.run(str(tmp_path / "in.zarr"), str(tmp_path / "store"), log=lambda *x: None,
+               device_resident=False, **kw)
+    assert all(st.get("device_resident") for st in a["stats"])
+    assert not any(st.get("device_resident") for st in b["stats"])
+    assert a["levels"] == b["levels"] >= 4
+    for lvl in range(a["levels"] + 1):
+        pa, pb = tmp_path / "dev" / str(lvl), tmp_path / "store" / str(lvl)
+        assert np.array_equal(S.read_array(pa), S.read_array(pb)), lvl
+        assert S.open_array(pa).metadata == S.open_array(pb).metadata
+    with open(tmp_path / "dev" / "zarr.json") as f, open(tmp_path / "store" / "zarr.json") as g:
+        assert json.load(f) == json.load(g)

@@ -230,6 +230,21 @@ def _nbytes(shape, data_type) -> int:
     return n * S.NUMPY[data_type]().itemsize
 
 
+def to_device(host, data_type: str, device: int):
+    """A host array read from a store (bfloat16 as raw uint16) as a device tensor of its type."""
+    import torch
+    x = torch.from_numpy(host).to(torch.device("cuda", device))
+    return x.view(torch.bfloat16) if data_type == "bfloat16" else x
+
+
+def to_host(x):
+    """A device tensor as the host array store.write_array takes (bfloat16 as raw uint16)."""
+    import torch
+    if x.dtype == torch.bfloat16:
+        x = x.view(torch.uint16)
+    return x.cpu().numpy()
+
+
 def run_device_chain(steps: list, paths: list, device: int = 0, nthreads: int = 0,
                      log=print, budget_frac: float = 0.8):
     """Run steps[0..] device-resident: paths[k] is step k's input path (paths[k+1] its output).
@@ -260,7 +275,7 @@ def run_device_chain(steps: list, paths: list, device: int = 0, nthreads: int = 
     host = S.read_array(paths[0], nthreads=nthreads)
     t_read = time.perf_counter() - t0
     dev = torch.device("cuda", device)
-    x = torch.from_numpy(host).to(dev)
+    x = to_device(host, src_info.data_type, device)
     x_dt, x_chunk = src_info.data_type, src_info.chunk_shape
     ctx = F.default_context(device)
     for k, step in enumerate(steps):
@@ -280,7 +295,7 @@ def run_device_chain(steps: list, paths: list, device: int = 0, nthreads: int = 
                         "threads": nthreads, "device_resident": True})
         x, x_dt, x_chunk = y, out_info.data_type, out_info.chunk_shape
     t2 = time.perf_counter()
-    out_host = x.cpu().numpy()
+    out_host = to_host(x)
     S.write_array(paths[-1], out_host, nthreads=nthreads)
     results[-1]["encode_s"] = time.perf_counter() - t2
     return results

@@ -12,7 +12,10 @@ Follows src/bin/zarrs_ome.rs (0.7.2):
 * level 0 is a copy of the input, or with any reencoding argument (ZarrReencodingArgs,
   lib.rs:274-377) the input reencoded into the new encoding (:341-366);
 * array 0's attributes move to the group, without "_zarrs" (:368-377);
-* level i is the downsample of level i-1 read back from the output (:515-738). Its encoding is the
+* level i is the downsample of level i-1 (:515-738): read back from the output store as the
+  reference does, or — when level 0 and its pyramid fit 80 % of the free device memory
+  (`--no-device-resident` turns it off) — computed from the previous level kept in HBM, level 0
+  read once and every level written once (the same kernels, so the same bits). Its encoding is the
   input's with zarrs_ome's per-level shapes (:528-560): a sharded input gets the shard shape
   min(shard, output) and the inner chunk min(inner chunk, output); otherwise the chunk shape
   min(chunk, output), which get_array_builder_reencode applies only to sharded outputs
@@ -43,7 +46,8 @@ import numpy as np
 
 from . import _abi
 from . import store as S
-from .zarrs_filter import REENCODE_KEYS, _add_reencode_args, encoding_of
+from .zarrs_filter import (REENCODE_KEYS, _add_reencode_args, _device_ok, encoding_of,
+                           to_device, to_host)
 
 VERSION = "zarrs_tools_amd 0.2 (MI355X)"
 
@@ -80,6 +84,8 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--group-attributes", default=None)
     ap.add_argument("--exists", choices=["erase", "exit", "overwrite"], default="erase")
     ap.add_argument("--device", type=int, default=0)
+    ap.add_argument("--no-device-resident", action="store_true",
+                    help="read every level back from the store (the reference's loop)")
     _add_reencode_args(ap)  # adds --chunk-limit too
     return ap
 
@@ -136,10 +142,21 @@ def _reencode_level0(src, dst, encoding, nthreads, log):
     log(f"0: reencode {src} -> {dst} ({out.data_type} {list(out.shape)})")
 
 
+def _device_pyramid_fits(info, gauss, device: int, frac: float = 0.8) -> bool:
+    """Level 0 + the pyramid (< 1/7 of level 0 for 2x factors, bounded by level 0 here) + the
+    f32 Gaussian of the largest level, against `frac` of the free device memory."""
+    import torch
+    n = int(np.prod(info.shape))
+    need = 2 * n * S.NUMPY[info.data_type]().itemsize + (4 * n if gauss is not None else 0)
+    free, _ = torch.cuda.mem_get_info(device)
+    return need <= frac * free
+
+
 def run(input_path, output_path, factor=None, max_levels: int = 10, discrete: bool = False,
         name=None, exists: str = "erase", device: int = 0, nthreads: int = 0,
         gaussian_sigma=None, gaussian_kernel_half_size=None, physical_size=None,
-        physical_units=None, group_attributes=None, reencoding=None, log=print) -> dict:
+        physical_units=None, group_attributes=None, reencoding=None, log=print,
+        device_resident: bool = True) -> dict:
     t0 = time.perf_counter()
     info = S.open_array(input_path)
     nd = info.ndim
@@ -195,12 +212,41 @@ def run(input_path, output_path, factor=None, max_levels: int = 10, discrete: bo
         {"type": "scale", "scale": list(scale)}]}]
     shape = list(S.open_array(lvl0).shape)
     stats = []
+    lvl0_info = S.open_array(lvl0)
+    on_device = (device_resident and _device_ok(device)
+                 and _device_pyramid_fits(lvl0_info, gauss, device))
+    cur = None  # the previous level in HBM (device-resident pyramid)
+    if on_device:
+        from . import filter as F
+        ctx = F.default_context(device)
+        t1 = time.perf_counter()
+        cur = to_device(S.read_array(lvl0, nthreads=nthreads), lvl0_info.data_type, device)
+        log(f"   level 0 -> device in {time.perf_counter() - t1:.2f}s")
     for i in range(1, max_levels + 1):
         src, dst = os.path.join(output_path, str(i - 1)), os.path.join(output_path, str(i))
         src_info = S.open_array(src)
         out_shape = [max(s // f, 1) for s, f in zip(shape, factor)]  # downsample.rs:162-168
         enc = level_encoding(src_info, out_shape)
-        if gauss is not None:
+        if on_device:
+            # the level from the previous one in HBM: (Gaussian, f32) then the downsample, the
+            # same kernels as the store path's per-row calls (chunked == whole array)
+            t1 = time.perf_counter()
+            S.create_output(src, dst, None, out_shape, enc)
+            v = cur
+            if gauss is not None:
+                v = F.Gaussian(gauss[0], gauss[1]).apply_ndarray(v, dtype_out="float32", ctx=ctx)
+            ds = F.Downsample(factor, discrete=discrete)
+            nxt = ds._apply(v, src_info.data_type, discrete, ctx)
+            nxt = nxt.reshape(out_shape)
+            ctx.synchronize()
+            t_k = time.perf_counter() - t1
+            t2 = time.perf_counter()
+            S.write_array(dst, to_host(nxt), nthreads=nthreads)
+            st = {"wall_s": time.perf_counter() - t1, "decode_s": 0.0,
+                  "encode_s": time.perf_counter() - t2, "h2d_s": 0.0, "kernel_s": t_k,
+                  "d2h_s": 0.0, "voxels": int(nxt.numel()), "device_resident": True}
+            cur = nxt
+        elif gauss is not None:
             st = S.downsample_gaussian(src, dst, factor, gauss[0], gauss[1], device=device,
                                        nthreads=nthreads, encoding=enc)
         else:
@@ -244,7 +290,8 @@ def main(argv=None) -> int:
     try:
         run(a.input, a.output, a.factor, a.max_levels, a.discrete, a.name, a.exists, a.device,
             a.filter_chunk_limit or 0, a.gaussian_sigma, a.gaussian_kernel_half_size,
-            a.physical_size, a.physical_units, a.group_attributes, enc)
+            a.physical_size, a.physical_units, a.group_attributes, enc,
+            device_resident=not a.no_device_resident)
     except _abi.FilterError as e:
         print(f"Error: {e}", file=sys.stderr)
         return 1
