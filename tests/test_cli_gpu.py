@@ -254,3 +254,28 @@ def test_zarrs_ome_device_resident_equals_store_levels(tmp_path, mode):
         assert S.open_array(pa).metadata == S.open_array(pb).metadata
     with open(tmp_path / "dev" / "zarr.json") as f, open(tmp_path / "store" / "zarr.json") as g:
         assert json.load(f) == json.load(g)
+
+
+def test_store_step_split_over_processes_equals_one_process(tmp_path):
+    """zarrs_filter --gpus N: each store step split by output chunk rows over N processes (one
+    per GPU; rehearsed here with every process on device 0) gives the one-process output, and
+    zarr.json is written once at the end."""
+    shape, chunk = (12, 20, 24, 40), (4, 8, 8, 16)  # 4-D: rows along t (config T's split)
+    v = O.synth_step_noise_f32(shape)
+    S.create_array(tmp_path / "in.zarr", "float32", shape, chunk)
+    S.write_array(tmp_path / "in.zarr", v)
+    steps = lambda out: [  # noqa: E731
+        {"filter": "guided_filter", "input": str(tmp_path / "in.zarr"), "output": "$g",
+         "epsilon": 2500.0, "radius": 2},
+        {"filter": "downsample", "input": "$g", "output": out, "stride": [1, 2, 2, 2]},
+    ]
+    one = ZF.run(steps(str(tmp_path / "one.zarr")), tmp=str(tmp_path), log=lambda *a: None,
+                 device_chain=False)
+    two = ZF.run(steps(str(tmp_path / "two.zarr")), tmp=str(tmp_path), log=lambda *a: None,
+                 gpus=2, gpu_devices=[0, 0])
+    assert all(st.get("processes") == 2 for st in two)
+    assert np.array_equal(S.read_array(tmp_path / "one.zarr"), S.read_array(tmp_path / "two.zarr"))
+    assert S.open_array(tmp_path / "one.zarr").metadata == S.open_array(tmp_path / "two.zarr").metadata
+    gf = O.guided_filter_apply(v, chunk, 2500.0, 2, nthreads=8)
+    want = O.downsample(gf, "float32", (1, 2, 2, 2), "float32")
+    assert rel_err(S.read_array(tmp_path / "one.zarr"), want) <= FLOAT_TOL

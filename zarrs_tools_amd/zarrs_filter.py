@@ -121,6 +121,9 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--chunk-limit", type=int, default=None)
     ap.add_argument("--device", type=int, default=0)
     ap.add_argument("--stats", action="store_true", help="print per-filter stats as JSON")
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="split every store step over this many GPUs (one process each) by "
+                         "output chunk rows")
     ap.add_argument("--no-device-chain", action="store_true",
                     help="run every step store -> store, also chains of temporaries")
     sub = ap.add_subparsers(dest="filter")
@@ -301,6 +304,48 @@ def run_device_chain(steps: list, paths: list, device: int = 0, nthreads: int = 
     return results
 
 
+def _rows_worker(name: str, src: str, dst: str, params: dict, device: int, rows, nthreads: int):
+    """One process of a multi-GPU store step: output chunk rows [rows[0], rows[1]) on `device`,
+    no metadata writes (the parent writes zarr.json once every row is done)."""
+    kw = dict(device=device, rows=rows, nthreads=nthreads, erase=False, finish=False,
+              encoding=params.get("encoding"), data_type=params.get("data_type"))
+    if name == "guided_filter":
+        return S.guided_filter(src, dst, params["epsilon"], params["radius"], **kw)
+    if name == "gaussian":
+        return S.gaussian(src, dst, params["sigma"], params["kernel_half_size"], **kw)
+    return S.downsample(src, dst, params["stride"], discrete=params["discrete"], **kw)
+
+
+def run_rows_parallel(name: str, src: str, dst: str, params: dict, out_shape, gpus: int,
+                      nthreads: int = 0, devices=None) -> dict:
+    """A store step split over `gpus` processes (one per GPU, guided_filter.rs:260-316's chunk
+    loop partitioned into contiguous output chunk rows along axis 0; no data exchange: each
+    process reads its rows' inputs with their halo). The output's zarr.json is written once, by
+    the parent, after every process finished (zarrs_filter.rs:297-313). `devices` maps process
+    g to a device (default g; a 1-GPU rehearsal passes [0] * gpus)."""
+    import multiprocessing as mp
+    from concurrent.futures import ProcessPoolExecutor
+    info = S.open_array(src)
+    S.create_output(src, dst, params.get("data_type"), out_shape, params.get("encoding"))
+    out = S.open_array(dst)
+    os.remove(os.path.join(dst, "zarr.json"))  # "not finished" until every row is written
+    nrows = -(-out.shape[0] // out.chunk_shape[0])
+    bounds = [(g * nrows // gpus, (g + 1) * nrows // gpus) for g in range(gpus)]
+    devices = devices or list(range(gpus))
+    per = max(1, (nthreads or min(16, os.cpu_count() or 1)) // gpus)
+    t0 = time.perf_counter()
+    with ProcessPoolExecutor(gpus, mp_context=mp.get_context("spawn")) as ex:
+        futs = [ex.submit(_rows_worker, name, src, dst, params, devices[g], bounds[g], per)
+                for g in range(gpus) if bounds[g][1] > bounds[g][0]]
+        parts = [f.result() for f in futs]
+    S.create_output(src, dst, params.get("data_type"), out_shape, params.get("encoding"))
+    st = {k: sum(p[k] for p in parts) for k in parts[0] if isinstance(parts[0][k], (int, float))}
+    st["wall_s"] = time.perf_counter() - t0
+    st["processes"] = len(parts)
+    del info
+    return st
+
+
 def _device_ok(device: int) -> bool:
     try:
         import torch
@@ -311,8 +356,12 @@ def _device_ok(device: int) -> bool:
 
 def run(steps: list, exists: str = "erase", tmp: str | None = None,
         chunk_limit: int | None = None, device: int = 0, stats: bool = False,
-        log=print, device_chain: bool = True) -> list:
-    """Run a list of filter steps (the run-config form); returns the per-step stats."""
+        log=print, device_chain: bool = True, gpus: int = 1, gpu_devices=None) -> list:
+    """Run a list of filter steps (the run-config form); returns the per-step stats. gpus > 1:
+    every store step is split over that many processes by output chunk rows (one per GPU;
+    `gpu_devices` maps process g to a device, default g); device-resident chains are then off."""
+    if gpus > 1:
+        device_chain = False
     tmp_root = tmp or tempfile.gettempdir()
     temps: dict[str, str] = {}
     made: list[str] = []
@@ -348,42 +397,37 @@ def run(steps: list, exists: str = "erase", tmp: str | None = None,
         name = step.get("filter")
         threads = step.get("chunk_limit") or chunk_limit or 0
         info = S.open_array(src)
+        f, out_shape, _dt = _step_params(step, info)
+        enc = encoding_of(step)
         if name == "guided_filter":
-            if "epsilon" not in step or "radius" not in step:
-                raise _abi.InvalidParameters(_abi.ERR_INVALID_PARAMETERS,
-                                             "guided_filter needs epsilon and radius")
-            log(f"{i}: guided_filter epsilon={step['epsilon']} radius={step['radius']} "
+            params = {"epsilon": float(step["epsilon"]), "radius": int(step["radius"])}
+            log(f"{i}: guided_filter epsilon={params['epsilon']} radius={params['radius']} "
                 f"{src} ({info.data_type} {list(info.shape)}) -> {dst}")
-            st = S.guided_filter(src, dst, float(step["epsilon"]), int(step["radius"]),
-                                 data_type=step.get("data_type"), device=device,
-                                 nthreads=threads, encoding=encoding_of(step))
         elif name == "gaussian":
-            sigma, half = step.get("sigma"), step.get("kernel_half_size")
-            if isinstance(sigma, str):
-                sigma = _parse_floats(sigma)
-            if isinstance(half, str):
-                half = _parse_stride(half)
-            if (not sigma or not half or len(sigma) != info.ndim
-                    or len(half) != info.ndim):
-                raise _abi.InvalidParameters(
-                    _abi.ERR_INVALID_PARAMETERS,
-                    "gaussian sigma and kernel_half_size need one entry per axis")
-            log(f"{i}: gaussian sigma={sigma} kernel_half_size={half} "
+            params = {"sigma": list(f.sigma), "kernel_half_size": list(f.kernel_half_size())}
+            log(f"{i}: gaussian sigma={params['sigma']} "
+                f"kernel_half_size={params['kernel_half_size']} "
                 f"{src} ({info.data_type} {list(info.shape)}) -> {dst}")
-            st = S.gaussian(src, dst, sigma, half, data_type=step.get("data_type"),
-                            device=device, nthreads=threads, encoding=encoding_of(step))
         else:
-            stride = step.get("stride")
-            if isinstance(stride, str):
-                stride = _parse_stride(stride)
-            if not stride or len(stride) != info.ndim:
-                raise _abi.InvalidParameters(_abi.ERR_INVALID_PARAMETERS,
-                                             "downsample stride must match the array rank")
-            log(f"{i}: downsample stride={stride} discrete={bool(step.get('discrete'))} "
+            params = {"stride": list(f.stride), "discrete": bool(step.get("discrete", False))}
+            log(f"{i}: downsample stride={params['stride']} discrete={params['discrete']} "
                 f"{src} ({info.data_type} {list(info.shape)}) -> {dst}")
-            st = S.downsample(src, dst, stride, discrete=bool(step.get("discrete", False)),
-                              data_type=step.get("data_type"), device=device,
-                              nthreads=threads, encoding=encoding_of(step))
+        params.update(data_type=step.get("data_type"), encoding=enc)
+        if gpus > 1:
+            st = run_rows_parallel(name, src, dst, params, out_shape, gpus, threads,
+                                   devices=gpu_devices)
+        elif name == "guided_filter":
+            st = S.guided_filter(src, dst, params["epsilon"], params["radius"],
+                                 data_type=params["data_type"], device=device,
+                                 nthreads=threads, encoding=enc)
+        elif name == "gaussian":
+            st = S.gaussian(src, dst, params["sigma"], params["kernel_half_size"],
+                            data_type=params["data_type"], device=device, nthreads=threads,
+                            encoding=enc)
+        else:
+            st = S.downsample(src, dst, params["stride"], discrete=params["discrete"],
+                              data_type=params["data_type"], device=device, nthreads=threads,
+                              encoding=enc)
         out = S.open_array(dst)
         log(f"   -> {out.data_type} {list(out.shape)} in {st['wall_s']:.2f}s "
             f"(rw:{st['decode_s']:.2f}/{st['encode_s']:.2f} p:{st['kernel_s']:.3f})")
@@ -457,7 +501,7 @@ def main(argv=None) -> int:
         return 2
     try:
         run(steps, a.exists, a.tmp, a.chunk_limit, a.device, a.stats,
-            device_chain=not a.no_device_chain)
+            device_chain=not a.no_device_chain, gpus=a.gpus)
     except _abi.FilterError as e:
         print(f"Error: {e}", file=sys.stderr)
         return 1
