@@ -103,12 +103,19 @@ def create_array(path, data_type: str, shape, chunk_shape, codecs: Optional[str]
     return open_array(path)
 
 
-def read_array(path, start=None, shape=None, nthreads: int = 0) -> np.ndarray:
-    """Array::retrieve_array_subset_ndarray into a numpy array (bfloat16 as raw uint16)."""
+def read_array(path, start=None, shape=None, nthreads: int = 0,
+               out: Optional[np.ndarray] = None) -> np.ndarray:
+    """Array::retrieve_array_subset_ndarray into a numpy array (bfloat16 as raw uint16); `out`:
+    an existing C-contiguous array of that shape and type to fill (e.g. a view of pinned host
+    memory)."""
     info = open_array(path)
     start = [0] * info.ndim if start is None else [int(s) for s in start]
     shape = list(info.shape) if shape is None else [int(s) for s in shape]
-    out = np.empty(shape, dtype=NUMPY[info.data_type])
+    if out is None:
+        out = np.empty(shape, dtype=NUMPY[info.data_type])
+    elif (list(out.shape) != shape or out.dtype != np.dtype(NUMPY[info.data_type])
+          or not out.flags["C_CONTIGUOUS"]):
+        raise _abi.InvalidParameters(_abi.ERR_INVALID_PARAMETERS, "read_array: bad out array")
     check(lib().zt_store_read_subset(_b(path), i64_array(start), i64_array(shape),
                                      out.ctypes.data_as(ctypes.c_void_p), int(nthreads)))
     return out

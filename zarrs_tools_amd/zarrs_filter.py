@@ -233,19 +233,29 @@ def _nbytes(shape, data_type) -> int:
     return n * S.NUMPY[data_type]().itemsize
 
 
-def to_device(host, data_type: str, device: int):
-    """A host array read from a store (bfloat16 as raw uint16) as a device tensor of its type."""
+def read_to_device(path, device: int, nthreads: int = 0):
+    """A whole store array decoded straight into pinned host memory and copied to the device at
+    pinned-transfer speed; bfloat16 arrays come back as torch.bfloat16."""
     import torch
-    x = torch.from_numpy(host).to(torch.device("cuda", device))
-    return x.view(torch.bfloat16) if data_type == "bfloat16" else x
+    from . import filter as F
+    info = S.open_array(path)
+    store_dt = "uint16" if info.data_type == "bfloat16" else info.data_type
+    host = torch.empty(tuple(info.shape), dtype=F.torch_dtype(store_dt), pin_memory=True)
+    S.read_array(path, nthreads=nthreads, out=host.numpy())
+    x = host.to(torch.device("cuda", device), non_blocking=True)
+    torch.cuda.synchronize(device)
+    del host
+    return x.view(torch.bfloat16) if info.data_type == "bfloat16" else x
 
 
-def to_host(x):
-    """A device tensor as the host array store.write_array takes (bfloat16 as raw uint16)."""
+def write_from_device(path, x, nthreads: int = 0) -> None:
+    """A device tensor (the whole array at `path`) through pinned host memory into the store."""
     import torch
     if x.dtype == torch.bfloat16:
         x = x.view(torch.uint16)
-    return x.cpu().numpy()
+    host = torch.empty(tuple(x.shape), dtype=x.dtype, pin_memory=True)
+    host.copy_(x)
+    S.write_array(path, host.numpy(), nthreads=nthreads)
 
 
 def run_device_chain(steps: list, paths: list, device: int = 0, nthreads: int = 0,
@@ -275,10 +285,9 @@ def run_device_chain(steps: list, paths: list, device: int = 0, nthreads: int = 
         S.create_output(paths[k], paths[k + 1], odt, oshape, encoding_of(step))
     t0 = time.perf_counter()
     src_info = S.open_array(paths[0])
-    host = S.read_array(paths[0], nthreads=nthreads)
+    x = read_to_device(paths[0], device, nthreads)
     t_read = time.perf_counter() - t0
     dev = torch.device("cuda", device)
-    x = to_device(host, src_info.data_type, device)
     x_dt, x_chunk = src_info.data_type, src_info.chunk_shape
     ctx = F.default_context(device)
     for k, step in enumerate(steps):
@@ -298,8 +307,7 @@ def run_device_chain(steps: list, paths: list, device: int = 0, nthreads: int = 
                         "threads": nthreads, "device_resident": True})
         x, x_dt, x_chunk = y, out_info.data_type, out_info.chunk_shape
     t2 = time.perf_counter()
-    out_host = to_host(x)
-    S.write_array(paths[-1], out_host, nthreads=nthreads)
+    write_from_device(paths[-1], x, nthreads)
     results[-1]["encode_s"] = time.perf_counter() - t2
     return results
 

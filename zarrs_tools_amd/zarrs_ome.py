@@ -47,7 +47,7 @@ import numpy as np
 from . import _abi
 from . import store as S
 from .zarrs_filter import (REENCODE_KEYS, _add_reencode_args, _device_ok, encoding_of,
-                           to_device, to_host)
+                           read_to_device, write_from_device)
 
 VERSION = "zarrs_tools_amd 0.2 (MI355X)"
 
@@ -220,7 +220,7 @@ def run(input_path, output_path, factor=None, max_levels: int = 10, discrete: bo
         from . import filter as F
         ctx = F.default_context(device)
         t1 = time.perf_counter()
-        cur = to_device(S.read_array(lvl0, nthreads=nthreads), lvl0_info.data_type, device)
+        cur = read_to_device(lvl0, device, nthreads)
         log(f"   level 0 -> device in {time.perf_counter() - t1:.2f}s")
     for i in range(1, max_levels + 1):
         src, dst = os.path.join(output_path, str(i - 1)), os.path.join(output_path, str(i))
@@ -241,7 +241,7 @@ def run(input_path, output_path, factor=None, max_levels: int = 10, discrete: bo
             ctx.synchronize()
             t_k = time.perf_counter() - t1
             t2 = time.perf_counter()
-            S.write_array(dst, to_host(nxt), nthreads=nthreads)
+            write_from_device(dst, nxt, nthreads)
             st = {"wall_s": time.perf_counter() - t1, "decode_s": 0.0,
                   "encode_s": time.perf_counter() - t2, "h2d_s": 0.0, "kernel_s": t_k,
                   "d2h_s": 0.0, "voxels": int(nxt.numel()), "device_resident": True}
