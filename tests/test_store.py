@@ -131,3 +131,102 @@ def test_errors_are_filter_errors(tmp_path):
     with pytest.raises(_abi.FilterError):
         S.write_array(S.create_array(tmp_path / "w.zarr", "uint8", (4,), (2,)).path,
                       np.zeros(3, np.uint8), start=(1,))  # not chunk aligned
+
+
+# ---- byte layouts pinned against the Zarr V3 specification and independent decoders ----------
+# (the reference ships no store fixtures; these check the chunks this store writes with decoders
+# that share no code with it: Python's gzip / zlib, a table-free crc32c, libzstd through ctypes)
+
+def _crc32c(data: bytes) -> int:
+    """CRC-32C (Castagnoli, reflected polynomial 0x82F63B78), bit by bit."""
+    crc = 0xFFFFFFFF
+    for b in data:
+        crc ^= b
+        for _ in range(8):
+            crc = (crc >> 1) ^ (0x82F63B78 if crc & 1 else 0)
+    return crc ^ 0xFFFFFFFF
+
+
+def test_crc32c_reference_value():
+    assert _crc32c(b"123456789") == 0xE3069283  # the CRC-32C check value
+
+
+def _chunk(data, idx, chunk):
+    sl = tuple(slice(i * c, (i + 1) * c) for i, c in zip(idx, chunk))
+    blk = data[sl]
+    out = np.zeros(chunk, data.dtype)  # edge chunks are padded with the fill value (0)
+    out[tuple(slice(0, n) for n in blk.shape)] = blk
+    return out
+
+
+def test_gzip_chunks_decode_with_python_gzip(tmp_path):
+    import gzip
+    shape, chunk = (10, 12), (8, 8)
+    p = tmp_path / "g.zarr"
+    S.create_array(p, "int16", shape, chunk, S.codecs_json("gzip", 6))
+    data = np.arange(120, dtype=np.int16).reshape(shape) * 7 - 300
+    S.write_array(p, data)
+    for i in range(2):
+        for j in range(2):
+            raw = gzip.decompress((p / "c" / str(i) / str(j)).read_bytes())
+            assert raw == _chunk(data, (i, j), chunk).astype("<i2").tobytes()
+
+
+def test_zstd_chunks_decode_with_libzstd(tmp_path):
+    import ctypes
+    import ctypes.util
+    if not S.codec_available("zstd"):
+        pytest.skip("libzstd.so.1 not present")
+    z = ctypes.CDLL(ctypes.util.find_library("zstd") or "libzstd.so.1")
+    z.ZSTD_decompress.restype = ctypes.c_size_t
+    z.ZSTD_decompress.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+                                  ctypes.c_size_t]
+    z.ZSTD_isError.argtypes = [ctypes.c_size_t]
+    shape, chunk = (9, 9), (9, 9)
+    p = tmp_path / "z.zarr"
+    S.create_array(p, "float32", shape, chunk, S.codecs_json("zstd", 3))
+    data = np.linspace(-4, 4, 81, dtype=np.float32).reshape(shape)
+    S.write_array(p, data)
+    comp = (p / "c" / "0" / "0").read_bytes()
+    assert comp[:4] == b"\x28\xb5\x2f\xfd"  # zstd frame magic
+    out = ctypes.create_string_buffer(data.nbytes)
+    n = z.ZSTD_decompress(out, data.nbytes, comp, len(comp))
+    assert not z.ZSTD_isError(n) and n == data.nbytes
+    assert out.raw == data.astype("<f4").tobytes()
+
+
+def test_sharding_layout_per_spec(tmp_path):
+    """sharding_indexed, index at the end: n inner chunks x (offset u64 LE, nbytes u64 LE), the
+    index bytes followed by their crc32c (u32 LE); empty inner chunks are (2^64-1, 2^64-1)."""
+    import struct
+    p = tmp_path / "s.zarr"
+    inner = (4, 4)
+    S.create_array(p, "uint16", (8, 8), (8, 8), S.codecs_json(shard_inner=inner))
+    data = np.arange(64, dtype=np.uint16).reshape(8, 8)
+    data[4:, 4:] = 0  # may be stored as an empty inner chunk (all fill value)
+    S.write_array(p, data)
+    raw = (p / "c" / "0" / "0").read_bytes()
+    n = 4
+    index = raw[-(16 * n + 4):-4]
+    assert struct.unpack("<I", raw[-4:])[0] == _crc32c(index)
+    for k in range(n):
+        off, nb = struct.unpack("<QQ", index[16 * k:16 * k + 16])
+        i, j = divmod(k, 2)  # C order over the inner chunk grid
+        want = _chunk(data, (i, j), inner)
+        if off == 2 ** 64 - 1:
+            assert nb == 2 ** 64 - 1 and not want.any()
+            continue
+        assert raw[off:off + nb] == want.astype("<u2").tobytes()
+
+
+def test_crc32c_codec_appends_checksum(tmp_path):
+    import struct
+    p = tmp_path / "c.zarr"
+    chain = json.dumps([{"name": "bytes", "configuration": {"endian": "little"}},
+                        {"name": "crc32c"}])
+    S.create_array(p, "uint8", (16,), (16,), chain)
+    data = np.arange(16, dtype=np.uint8) * 3
+    S.write_array(p, data)
+    raw = (p / "c" / "0").read_bytes()
+    assert raw[:-4] == data.tobytes()
+    assert struct.unpack("<I", raw[-4:])[0] == _crc32c(data.tobytes())
