@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <type_traits>
 
 #include "zt_device.hpp"
@@ -421,12 +422,15 @@ hipError_t launch_fused4(G4FParams p, hipStream_t s) {
     const int64_t gx = tiles * nseg;
     if (gx > 0x7FFFFFFF) return hipErrorInvalidValue;
     auto kern = g4_fused_kernel<R, TOut>;
-    static bool attr = false;  // > 64 KB of dynamic LDS needs the opt-in
-    if (!attr) {
+    // > 64 KB of dynamic LDS needs the opt-in, once per device (a bit per device)
+    static std::atomic<uint64_t> attr{0};
+    int dev = 0;
+    if (hipError_t e = hipGetDevice(&dev)) return e;
+    if (!(attr.load(std::memory_order_relaxed) & (1ull << (dev & 63)))) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
         if (e != hipSuccess) return e;
-        attr = true;
+        attr.fetch_or(1ull << (dev & 63), std::memory_order_relaxed);
     }
     hipLaunchKernelGGL(kern, dim3((unsigned)gx), dim3(C::NT), C::LDS, s, p);
     return hipGetLastError();

@@ -4,6 +4,8 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+
+#include <atomic>
 #include <stdint.h>
 
 #include <algorithm>
@@ -1283,18 +1285,31 @@ inline void interior_tiles(long long o0, long long o_end, long long n, int T, in
     hi = (int)h;
 }
 
+// > 64 KB of dynamic LDS needs the per-function opt-in, once per (kernel, device): a bit per
+// device in a per-instantiation mask (one process may drive several devices).
+template <typename K>
+inline std::atomic<uint64_t>& attr_devices() {
+    static std::atomic<uint64_t> mask{0};
+    return mask;
+}
+inline hipError_t allow_dynamic_lds(const void* kern, int bytes, std::atomic<uint64_t>& mask) {
+    int dev = 0;
+    if (hipError_t e = hipGetDevice(&dev)) return e;
+    const uint64_t bit = 1ull << (dev & 63);
+    if (mask.load(std::memory_order_relaxed) & bit) return hipSuccess;
+    if (hipError_t e = hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, bytes))
+        return e;
+    mask.fetch_or(bit, std::memory_order_relaxed);
+    return hipSuccess;
+}
+
 template <int R, int TY, int NT, typename TIn, typename TOut, bool EDGE, int ABL = 0>
 inline hipError_t launch_fused_variant(const GFParams& p, long long nwg, hipStream_t stream) {
     using C = GFConfig<R, TY, NT>;
     const size_t lds = (size_t)C::LDS_BYTES;
     auto kern = gf3d_fused_kernel<R, TY, NT, TIn, TOut, EDGE, ABL>;
-    static bool attr_set = false;  // per instantiation
-    if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)kern,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (e != hipSuccess) return e;
-        attr_set = true;
-    }
+    if (hipError_t e = allow_dynamic_lds((const void*)kern, (int)lds, attr_devices<decltype(kern)>()))
+        return e;
     if (nwg <= 0) return hipSuccess;
     if (nwg > 0x7FFFFFFFLL) return hipErrorInvalidValue;
     hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(NT), lds, stream, p);

@@ -162,8 +162,8 @@ template <int TMAX>
 __global__ __launch_bounds__(256) void g4_pointwise_kernel(const double* __restrict__ U3,
                                                            const float* __restrict__ v,
                                                            float2* __restrict__ AB, int T,
-                                                           int nz, int ny, int nx, int r,
-                                                           float eps) {
+                                                           int ta_ab, int tb_ab, int nz, int ny,
+                                                           int nx, int r, float eps) {
     const int64_t vol = (int64_t)nz * ny * nx;
     const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
     if (x >= nx) return;
@@ -176,7 +176,7 @@ __global__ __launch_bounds__(256) void g4_pointwise_kernel(const double* __restr
         for (int t = 0; t < TMAX; ++t) U[t] = t < T ? U3[t * vol + i] : 0.0;
 #pragma unroll
         for (int t = 0; t < TMAX; ++t) {
-            if (t >= T) continue;
+            if (t >= T || t < ta_ab || t >= tb_ab) continue;  // only the (a, b) K4 reads
             double U4 = 0.0;
             const int ta = max(t - r, 0), tb = min(t + r, T - 1);
 #pragma unroll
@@ -307,19 +307,27 @@ hipError_t launch_guided4d(const void* in, int dtype_in, void* out, int dtype_ou
     e = launch_box3_r<float, double, double>(radius, v, U3, T, nz, ny, nx, s);
     if (e != hipSuccess) return e;
     if (ny > 65535 || g.out_shape[2] > 65535) return hipErrorInvalidValue;  // grid.y
+    // (a, b) are needed only within R timepoints of the output's (a slab's halo timepoints
+    // beyond that feed stage 1 alone)
+    const int ta_ab = std::max<int>(0, (int)g.out_start[0] - radius);
+    const int tb_ab = std::min<int>(T, (int)(g.out_start[0] + g.out_shape[0]) + radius);
     const dim3 pgrid((unsigned)((nx + 255) / 256), (unsigned)ny,
                      (unsigned)std::min<int64_t>(nz, std::max<int64_t>(1, 65536 / ((int64_t)ny * ((nx + 255) / 256)) + 1)));
     if (T <= 4)
-        hipLaunchKernelGGL(g4_pointwise_kernel<4>, pgrid, dim3(256), 0, s, U3, v, AB, T, nz, ny,
-                           nx, radius, eps);
+        hipLaunchKernelGGL(g4_pointwise_kernel<4>, pgrid, dim3(256), 0, s, U3, v, AB, T, ta_ab,
+                           tb_ab, nz, ny, nx, radius, eps);
     else if (T <= 16)
-        hipLaunchKernelGGL(g4_pointwise_kernel<16>, pgrid, dim3(256), 0, s, U3, v, AB, T, nz,
-                           ny, nx, radius, eps);
+        hipLaunchKernelGGL(g4_pointwise_kernel<16>, pgrid, dim3(256), 0, s, U3, v, AB, T, ta_ab,
+                           tb_ab, nz, ny, nx, radius, eps);
     else
         return hipErrorInvalidValue;
     if ((e = hipGetLastError()) != hipSuccess) return e;
     float2* S3 = reinterpret_cast<float2*>(U3);
-    e = launch_box3_r<float2, dd2, float2>(radius, AB, S3, T, nz, ny, nx, s);
+    {  // K3 on the timepoints whose (a, b) sums K4 reads
+        const int64_t vol = (int64_t)nz * ny * nx;
+        e = launch_box3_r<float2, dd2, float2>(radius, AB + ta_ab * vol, S3 + ta_ab * vol,
+                                               tb_ab - ta_ab, nz, ny, nx, s);
+    }
     if (e != hipSuccess) return e;
     const int64_t onx = g.out_shape[3], ony = g.out_shape[2], onz = g.out_shape[1];
     const dim3 fgrid((unsigned)((onx + 255) / 256), (unsigned)ony,
