@@ -14,6 +14,12 @@ using namespace zt;
 #ifndef TK_ABL
 #define TK_ABL 0
 #endif
+#ifndef TK_TY
+#define TK_TY 32
+#endif
+#ifndef TK_NT
+#define TK_NT 1024
+#endif
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { \
     printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
@@ -39,10 +45,10 @@ int main(int argc, char** argv) {
     hipEvent_t a, b;
     CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
     std::vector<float> t;
-    CK((launch_fused_cfg<4, 32, 1024, float, float, TK_ABL>(p, s)));
+    CK((launch_fused_cfg<4, TK_TY, TK_NT, float, float, TK_ABL>(p, s)));
     for (int r = 0; r < 5; ++r) {
         CK(hipEventRecord(a, s));
-        CK((launch_fused_cfg<4, 32, 1024, float, float, TK_ABL>(p, s)));
+        CK((launch_fused_cfg<4, TK_TY, TK_NT, float, float, TK_ABL>(p, s)));
         CK(hipEventRecord(b, s));
         CK(hipEventSynchronize(b));
         float ms; CK(hipEventElapsedTime(&ms, a, b));

@@ -332,13 +332,48 @@ __device__ __forceinline__ void static_for(F&& f) {
     }
 }
 
+// Buffer (SRD) access for the march: the slice base goes in a wave-uniform descriptor, each
+// point keeps a 32-bit byte offset, and an offset past num_records reads 0 / drops the store,
+// so the march has no branches around its memory instructions: hipcc's vmcnt accounting then
+// waits for exactly the step-old prefetch, instead of draining every load (a guarded prefetch
+// and __syncthreads() each forced vmcnt(0) per step).
+using zrsrc_t = __amdgpu_buffer_rsrc_t;
+constexpr int kZBad = (int)0x80000000;
+__device__ __forceinline__ zrsrc_t z_rsrc(const void* base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes,
+                                             0x00020000);
+}
+template <typename T>
+__device__ __forceinline__ float z_load(zrsrc_t r, int off) {
+    if constexpr (sizeof(T) == 1) {
+        const uint8_t b = __builtin_amdgcn_raw_buffer_load_b8(r, off, 0, 0);
+        return Elem<T>::to_f32(__builtin_bit_cast(T, b));
+    } else if constexpr (sizeof(T) == 2) {
+        const uint16_t b = __builtin_amdgcn_raw_buffer_load_b16(r, off, 0, 0);
+        return Elem<T>::to_f32(__builtin_bit_cast(T, b));
+    } else if constexpr (sizeof(T) == 4) {
+        const uint32_t b = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
+        return Elem<T>::to_f32(__builtin_bit_cast(T, b));
+    } else {
+        typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+        const u2 b = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+        return Elem<T>::to_f32(__builtin_bit_cast(T, b));
+    }
+}
+// LDS hand-off barrier that leaves the global prefetches in flight (see gf_fused.hpp)
+__device__ __forceinline__ void z_lds_barrier() {
+    __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 template <int L, typename TIn>
 __global__ __launch_bounds__(256) void gauss_zyx_kernel(const TIn* __restrict__ in,
                                                         float* __restrict__ out, GaussZYX p,
                                                         int tiles_x, int tiles_y, int zseg) {
     constexpr int TY = kZYXTy, TX = kZYXTx, TH = TY + L - 1, TW = TX + L - 1, MID = L / 2;
     constexpr int NE = TH * TW, NPT = (NE + 255) / 256;
-    __shared__ float tile[TH * TW];
+    constexpr int NYI = TW * (TY / 4), NXI = TY * (TX / 4);  // y / x pass items
+    constexpr int NYP = (NYI + 255) / 256, NXP = (NXI + 255) / 256;
+    __shared__ float tile[NPT * 256];  // (rows past NE: the dummy writes of idle points)
     __shared__ float ybuf[TY * TW];
     const int tid = threadIdx.x;
     const int64_t nz = p.n[0], ny = p.n[1], nx = p.n[2];
@@ -355,7 +390,10 @@ __global__ __launch_bounds__(256) void gauss_zyx_kernel(const TIn* __restrict__ 
     const int hx = (int)(onx - x0 < TX ? onx - x0 : TX);
     const int64_t qy0 = p.o0[1] + y0 - MID, qx0 = p.o0[2] + x0 - MID;
     const int64_t plane = ny * nx;
-    int off[NPT];  // plane offset of each owned tile point (clamped, as the y / x passes clamp)
+    const uint32_t plane_bytes = (uint32_t)(plane * (int64_t)sizeof(TIn));
+    const uint32_t oplane_bytes = (uint32_t)(ony * onx * 4);
+    int off[NPT];  // byte offset in the plane of each owned tile point (clamped, as the y / x
+                   // passes clamp)
 #pragma unroll
     for (int k = 0; k < NPT; ++k) {
         const int e = tid + 256 * k;
@@ -363,15 +401,21 @@ __global__ __launch_bounds__(256) void gauss_zyx_kernel(const TIn* __restrict__ 
         int64_t qy = qy0 + r, qx = qx0 + c;
         qy = qy < 0 ? 0 : (qy > ny - 1 ? ny - 1 : qy);
         qx = qx < 0 ? 0 : (qx > nx - 1 ? nx - 1 : qx);
-        off[k] = e < NE ? (int)(qy * nx + qx) : 0;
+        off[k] = e < NE ? (int)((qy * nx + qx) * (int64_t)sizeof(TIn)) : kZBad;
     }
+    // x-pass items: output offset within the slice (kZBad for rows / quads outside the box);
+    // whole quads when the box width and the row pitch keep them inside and 16-byte aligned
+    const bool quads = (onx % 4 == 0) && (x0 % 4 == 0) && (((uintptr_t)out & 15) == 0);
     for (int64_t o = blockIdx.y; o < p.outer; o += gridDim.y) {
-        const TIn* vol = in + o * nz * plane;
-        auto ld = [&](int64_t zq, float (&v)[NPT]) {  // input slice zq (clamped) at the points
+        const char* vol = reinterpret_cast<const char*>(in) + o * nz * plane * (int64_t)sizeof(TIn);
+        auto slice = [&](int64_t zq) {  // input slice zq, clamped (wave-uniform)
             zq = zq < 0 ? 0 : (zq > nz - 1 ? nz - 1 : zq);
-            const TIn* sl = vol + zq * plane;
+            return z_rsrc(vol + zq * plane * (int64_t)sizeof(TIn), plane_bytes);
+        };
+        auto ld = [&](int64_t zq, float (&v)[NPT]) {
+            const zrsrc_t rs = slice(zq);
 #pragma unroll
-            for (int k = 0; k < NPT; ++k) v[k] = Elem<TIn>::to_f32(sl[off[k]]);
+            for (int k = 0; k < NPT; ++k) v[k] = z_load<TIn>(rs, off[k]);
         };
         float ring[L][NPT], pre[NPT];
         // window of the first output slice: position i = input slice o0 + kz0 + i - MID in slot
@@ -379,43 +423,55 @@ __global__ __launch_bounds__(256) void gauss_zyx_kernel(const TIn* __restrict__ 
 #pragma unroll
         for (int i = 0; i < L - 1; ++i) ld(p.o0[0] + kz0 + i - MID, ring[i]);
         ld(p.o0[0] + kz0 + L - 1 - MID, pre);
+        char* obase = reinterpret_cast<char*>(out) + o * onz * ony * onx * 4;
         for (int64_t kb = kz0; kb < kz1; kb += L) {
             static_for<0, L>([&](auto PH_) {
                 constexpr int PH = decltype(PH_)::value;
+                // no early exit: the last block of L steps runs whole (an exit here put a
+                // vmcnt(0) drain on the loop path); steps past the segment store nothing
                 const int64_t kz = kb + PH;
-                if (kz >= kz1) return;  // block-uniform
                 // slot of window position i at this phase: (PH + i) % L; position L - 1 is new
 #pragma unroll
                 for (int k = 0; k < NPT; ++k) ring[(PH + L - 1) % L][k] = pre[k];
-                if (kz + 1 < kz1) ld(p.o0[0] + kz + 1 + MID, pre);  // next step's entering slice
+                // next step's entering slice, unconditionally (clamped; unused past the segment)
+                ld(p.o0[0] + kz + 1 + MID, pre);
 #pragma unroll
                 for (int k = 0; k < NPT; ++k) {
                     float sum = -0.0f;  // Iterator::sum::<f32> (kernel.rs:46, :66)
 #pragma unroll
                     for (int i = 0; i < L; ++i) sum = sum + ring[(PH + i) % L][k] * p.w[0][i];
-                    if (tid + 256 * k < NE) tile[tid + 256 * k] = sum;
+                    tile[tid + 256 * k] = sum;
                 }
-                __syncthreads();
-                for (int item = tid; item < TW * (TY / 4); item += 256) {  // y pass, 4 rows
-                    const int c = item % TW, r0 = (item / TW) * 4;
-                    float v[4 + L - 1];
+                z_lds_barrier();
 #pragma unroll
-                    for (int j = 0; j < 4 + L - 1; ++j) v[j] = tile[(r0 + j) * TW + c];
+                for (int ip = 0; ip < NYP; ++ip) {  // y pass, 4 rows per item
+                    const int item = tid + 256 * ip;
+                    if (NYI % 256 == 0 || item < NYI) {
+                        const int c = item % TW, r0 = (item / TW) * 4;
+                        float v[4 + L - 1];
 #pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        float sum = -0.0f;
+                        for (int j = 0; j < 4 + L - 1; ++j) v[j] = tile[(r0 + j) * TW + c];
 #pragma unroll
-                        for (int i = 0; i < L; ++i) sum = sum + v[k + i] * p.w[1][i];
-                        ybuf[(r0 + k) * TW + c] = sum;
+                        for (int k = 0; k < 4; ++k) {
+                            float sum = -0.0f;
+#pragma unroll
+                            for (int i = 0; i < L; ++i) sum = sum + v[k + i] * p.w[1][i];
+                            ybuf[(r0 + k) * TW + c] = sum;
+                        }
                     }
                 }
-                __syncthreads();
-                for (int item = tid; item < TY * (TX / 4); item += 256) {  // x pass, 4 columns
+                z_lds_barrier();
+                const zrsrc_t ro =
+                    z_rsrc(obase + (kz < kz1 ? kz : 0) * ony * onx * 4, kz < kz1 ? oplane_bytes : 0u);
+#pragma unroll
+                for (int ip = 0; ip < NXP; ++ip) {  // x pass, 4 columns per item
+                    const int item = tid + 256 * ip;
                     const int r = item / (TX / 4), c0 = (item % (TX / 4)) * 4;
-                    if (r >= hy || c0 >= hx) continue;
+                    const bool live = (NXI % 256 == 0 || item < NXI) && r < hy;
                     float v[4 + L - 1];
 #pragma unroll
-                    for (int j = 0; j < 4 + L - 1; ++j) v[j] = ybuf[r * TW + c0 + j];
+                    for (int j = 0; j < 4 + L - 1; ++j)
+                        v[j] = ybuf[(live ? r : 0) * TW + c0 + j];
                     float o4[4];
 #pragma unroll
                     for (int k = 0; k < 4; ++k) {
@@ -424,28 +480,34 @@ __global__ __launch_bounds__(256) void gauss_zyx_kernel(const TIn* __restrict__ 
                         for (int i = 0; i < L; ++i) sum = sum + v[k + i] * p.w[2][i];
                         o4[k] = sum;
                     }
-                    float* dst = out + ((o * onz + kz) * ony + y0 + r) * onx + x0 + c0;
-                    if (c0 + 4 <= hx && ((uintptr_t)dst & 15) == 0) {
-                        typedef float v4f __attribute__((ext_vector_type(4)));
-                        const v4f q = {o4[0], o4[1], o4[2], o4[3]};
-                        __builtin_nontemporal_store(q, reinterpret_cast<v4f*>(dst));
+                    const int ooff = (int)(((y0 + r) * onx + x0 + c0) * 4);
+                    if (quads) {
+                        typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+                        const u4 q = {__float_as_uint(o4[0]), __float_as_uint(o4[1]),
+                                      __float_as_uint(o4[2]), __float_as_uint(o4[3])};
+                        __builtin_amdgcn_raw_buffer_store_b128(
+                            q, ro, live && c0 < hx ? ooff : kZBad, 0, 2);
                     } else {
 #pragma unroll
                         for (int k = 0; k < 4; ++k)
-                            if (c0 + k < hx) dst[k] = o4[k];
+                            __builtin_amdgcn_raw_buffer_store_b32(
+                                __float_as_uint(o4[k]), ro,
+                                live && c0 + k < hx ? ooff + 4 * k : kZBad, 0, 2);
                     }
                 }
                 // the next tile / ybuf writes follow this step's barriers (see gauss_yx_fast)
             });
         }
-        __syncthreads();  // the last step's reads of tile / ybuf before the next outer volume
+        z_lds_barrier();  // the last step's reads of tile / ybuf before the next outer volume
     }
 }
 
 bool gaussian_zyx_supported(const GaussZYX& p, int dtype_in) {
     (void)dtype_in;
+    // slices addressed by 32-bit byte offsets (buffer descriptors)
     return p.len >= 3 && p.len <= kGaussZYXMaxLen && p.len % 2 == 1 &&
-           p.n[1] * p.n[2] < 0x7FFFFFFF && (p.on[1] + kZYXTy - 1) / kZYXTy <= 0xFFFF &&
+           p.n[1] * p.n[2] * (int64_t)dtype_size(dtype_in) < 0x7FFFFFFF &&
+           p.on[1] * p.on[2] * 4 < 0x7FFFFFFF && (p.on[1] + kZYXTy - 1) / kZYXTy <= 0xFFFF &&
            (p.on[2] + kZYXTx - 1) / kZYXTx <= 0xFFFF;
 }
 

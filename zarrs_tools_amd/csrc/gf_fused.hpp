@@ -70,6 +70,15 @@
 #define GF_FASTDIV5 1  // stage-2 means as sum * RN(1/count) (one multiply; the sums already
                        // differ from the reference's f64 SAT sums by a few ulp)
 #endif
+#ifndef GF_PW_SYNC
+#define GF_PW_SYNC 0  // pointwise pairs advanced op by op (no s_nop between dependent v_pk_*)
+#endif
+#ifndef GF_TREE
+#define GF_TREE 1  // f64 window sums as a balanced tree + independent differences (short chains)
+#endif
+#ifndef GF_A_RCP
+#define GF_A_RCP 0  // a = s * rcp(s + eps) without Markstein's correction (<= 2 ulp)
+#endif
 
 namespace zt {
 
@@ -282,15 +291,35 @@ struct RingDispatch<W, W> {
 // ---------------------------------------------------------------------------------------------
 template <int R, int K>
 __device__ __forceinline__ void slide_sums_f64(const double (&in)[K + 2 * R], double (&out)[K]) {
-    double s = in[0];
+    if constexpr (GF_TREE) {
+        // exact sums: any association gives the same value, so the first window is a balanced
+        // tree and each later one adds an independently formed difference (chain depth
+        // log2(W) + K - 1 instead of 2R + 2(K - 1))
+        double c[2 * R + 1];
 #pragma unroll
-    for (int j = 1; j <= 2 * R; ++j) s += in[j];
-    out[0] = s;
+        for (int j = 0; j <= 2 * R; ++j) c[j] = in[j];
 #pragma unroll
-    for (int i = 1; i < K; ++i) {
-        s = s + in[i + 2 * R];
-        s = s - in[i - 1];
-        out[i] = s;
+        for (int w = 1; w <= 2 * R; w *= 2) {
+#pragma unroll
+            for (int j = 0; j + w <= 2 * R; j += 2 * w) c[j] = c[j] + c[j + w];
+        }
+        double d[K];
+#pragma unroll
+        for (int i = 1; i < K; ++i) d[i] = in[i + 2 * R] - in[i - 1];
+        out[0] = c[0];
+#pragma unroll
+        for (int i = 1; i < K; ++i) out[i] = out[i - 1] + d[i];
+    } else {
+        double s = in[0];
+#pragma unroll
+        for (int j = 1; j <= 2 * R; ++j) s += in[j];
+        out[0] = s;
+#pragma unroll
+        for (int i = 1; i < K; ++i) {
+            s = s + in[i + 2 * R];
+            s = s - in[i - 1];
+            out[i] = s;
+        }
     }
 }
 
@@ -529,7 +558,7 @@ struct GFConfig {
     static_assert(TX % K4 == 0, "P4 segment must divide the tile width");
     static_assert(N3 <= NT && N4 <= NT, "one work item per thread per phase");
     static_assert(RPW >= 1, "an E2 row fits one wave");
-    static_assert(NQC <= NT && NQ5 <= NT, "one staging quad per thread");
+    static_assert(GF_DIRECT || (NQC <= NT && NQ5 <= NT), "one staging quad per thread");
     static_assert(E2X % 4 == 0, "E2 rows are whole quads");
     static_assert(E2X % EPL == 0, "E2 rows are whole lane items");
     static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
@@ -829,28 +858,41 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     //   u = RN(RN(U) / c)   (summed_area_table_mean, exact: Markstein with rcp = RN(1/c))
     //   s = (v - u)^2;  a = s / (s + eps);  b = (1 - a) * u          (guided_filter.rs:126-137)
     constexpr int NP3 = C::K3 / 2;
+    // The compiler schedules the pairs as separate chains, each dependent v_pk_* then waiting on
+    // an s_nop; a scheduling fence after every op keeps them in lockstep instead (a fence, not
+    // an asm statement: the hazard recognizer pads after inline asm).
+    auto sync = [&](f2 (&)[NP3]) {
+        if constexpr (GF_PW_SYNC) __builtin_amdgcn_sched_barrier(0);
+    };
     auto pointwise = [&](const f2 (&Uf)[NP3], const f2 (&v)[NP3], const f2 (&fc)[NP3],
                          const f2 (&rc)[NP3], f2 (&a)[NP3], f2 (&bb)[NP3]) {
         f2 q[NP3], r[NP3], u[NP3], sq[NP3], den[NP3], y[NP3], e[NP3];
 #pragma unroll
         for (int k = 0; k < NP3; ++k) q[k] = Uf[k] * rc[k];
+        sync(q);
 #pragma unroll
         for (int k = 0; k < NP3; ++k) r[k] = pk_fma(-q[k], fc[k], Uf[k]);
+        sync(r);
 #pragma unroll
         for (int k = 0; k < NP3; ++k) u[k] = pk_fma(r[k], rc[k], q[k]);
+        sync(u);
 #pragma unroll
         for (int k = 0; k < NP3; ++k) sq[k] = v[k] - u[k];
+        sync(sq);
 #pragma unroll
         for (int k = 0; k < NP3; ++k) sq[k] = sq[k] * sq[k];  // (v - u).powf(2.0)
+        sync(sq);
         if constexpr (ABL & 32) {
 #pragma unroll
             for (int k = 0; k < NP3; ++k) { a[k] = sq[k]; bb[k] = u[k]; }
         } else {
 #pragma unroll
             for (int k = 0; k < NP3; ++k) den[k] = sq[k] + (f2){eps, eps};
+            sync(den);
 #pragma unroll
             for (int k = 0; k < NP3; ++k)
                 y[k] = (f2){__builtin_amdgcn_rcpf(den[k].x), __builtin_amdgcn_rcpf(den[k].y)};
+            sync(y);
             if constexpr (GF_NEWTON_A) {  // refine 1/den before Markstein's correction
 #pragma unroll
                 for (int k = 0; k < NP3; ++k) e[k] = pk_fma(-den[k], y[k], (f2){1.0f, 1.0f});
@@ -859,17 +901,29 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
             }
 #pragma unroll
             for (int k = 0; k < NP3; ++k) q[k] = sq[k] * y[k];
+            sync(q);
+            if constexpr (GF_A_RCP) {
 #pragma unroll
-            for (int k = 0; k < NP3; ++k) r[k] = pk_fma(-den[k], q[k], sq[k]);
+                for (int k = 0; k < NP3; ++k) a[k] = q[k];
+            } else {
 #pragma unroll
-            for (int k = 0; k < NP3; ++k) a[k] = pk_fma(r[k], y[k], q[k]);
+                for (int k = 0; k < NP3; ++k) r[k] = pk_fma(-den[k], q[k], sq[k]);
+                sync(r);
+#pragma unroll
+                for (int k = 0; k < NP3; ++k) a[k] = pk_fma(r[k], y[k], q[k]);
+                sync(a);
+            }
 #pragma unroll
             for (int k = 0; k < NP3; ++k) e[k] = (f2){1.0f, 1.0f} - a[k];
+            sync(e);
 #pragma unroll
             for (int k = 0; k < NP3; ++k) bb[k] = e[k] * u[k];
         }
     };
     static_assert(C::K3 % 2 == 0, "P3 works on pairs");
+    // every P3 segment lies inside the apron: unconditional Lab stores (a guard lets the compiler
+    // sink the second pair's pointwise chain into it, serialising the pairs)
+    constexpr bool kRowsWhole = C::E1Y % C::K3 == 0;
     auto do_p3 = [&](int tid, int zc) {  // y-window (f64) of Hx -> U; a, b -> Lab
         const int item = p3_item(tid);
         if (item < 0) return;
@@ -909,8 +963,8 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
 #pragma unroll
             for (int k = 0; k < NP3; ++k) {
                 const int ey = sg * C::K3 + 2 * k;
-                if (ey < C::E1Y) lab[ey * C::PA + col] = __builtin_shufflevector(a[k], bb[k], 0, 2);
-                if (ey + 1 < C::E1Y)
+                if (kRowsWhole || ey < C::E1Y) lab[ey * C::PA + col] = __builtin_shufflevector(a[k], bb[k], 0, 2);
+                if (kRowsWhole || ey + 1 < C::E1Y)
                     lab[(ey + 1) * C::PA + col] = __builtin_shufflevector(a[k], bb[k], 1, 3);
             }
             return;
@@ -932,8 +986,8 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
             const int gy = y0 - R + ey;
             // zero outside the domain: the clamped window sums of stage 2
             const bool ok0 = xzin && gy >= 0 && gy < ny, ok1 = xzin && gy + 1 >= 0 && gy + 1 < ny;
-            if (ey < C::E1Y) lab[ey * C::PA + col] = ok0 ? (f2){a[k].x, bb[k].x} : (f2){0.f, 0.f};
-            if (ey + 1 < C::E1Y)
+            if (kRowsWhole || ey < C::E1Y) lab[ey * C::PA + col] = ok0 ? (f2){a[k].x, bb[k].x} : (f2){0.f, 0.f};
+            if (kRowsWhole || ey + 1 < C::E1Y)
                 lab[(ey + 1) * C::PA + col] = ok1 ? (f2){a[k].y, bb[k].y} : (f2){0.f, 0.f};
         }
     };
