@@ -256,6 +256,7 @@ __global__ __launch_bounds__(G4FConfig<R>::NT) void g4_fused_kernel(G4FParams p)
         for (int t = 0; t < TS; ++t) v5[t] = ldv(t, zo, off5);
     };
     load_v5(zc_begin - R);
+    load_v3(zc_begin);  // S3's v of the first stage-1 slice; later slices a step ahead
 
     // count factors of the t-windows (clamped to the block's T)
     int ta_[TS], tb_[TS];
@@ -309,7 +310,8 @@ __global__ __launch_bounds__(G4FConfig<R>::NT) void g4_fused_kernel(G4FParams p)
             lds_barrier();
             // S3: y-window sums, t-window sums, pointwise stage -> Lab
             if (wave < (C::NI3 + 63) / 64 && i3 >= 0) {
-                load_v3(zc);  // L2 hits: the slice entered stage 1 R steps ago
+                // v3 = v of slice zc, loaded a step ago (outside any branch, so the wait here is
+                // for that load only, not a drain of this step's prefetches)
                 double U3[TS][C::KY3];
 #pragma unroll
                 for (int t = 0; t < TS; ++t) {
@@ -431,6 +433,7 @@ __global__ __launch_bounds__(G4FConfig<R>::NT) void g4_fused_kernel(G4FParams p)
                 }
             }
             load_v5(zo + 1);
+            load_v3(zc + 1);  // L2 hits: the slice entered stage 1 R steps ago
             // the next step's Z1 / Lab writes follow this step's S4 reads (third barrier); its X1
             // writes follow its first barrier, after every S5 read of Hab
         }

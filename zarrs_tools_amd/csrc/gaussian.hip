@@ -365,15 +365,50 @@ __device__ __forceinline__ void z_lds_barrier() {
     __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-template <int L, typename TIn>
+// 4 consecutive elements from one buffer access (16/8/4 bytes for 4/2/1-byte types)
+template <typename T>
+__device__ __forceinline__ void z_load4(zrsrc_t r, int off, float (&v)[4]) {
+    if constexpr (sizeof(T) == 4) {
+        typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+        const u4 q = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+        // elements copied out first: clang's bit_cast of a vector element lvalue reads element 0
+        const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = Elem<T>::to_f32(__builtin_bit_cast(T, w[e]));
+    } else if constexpr (sizeof(T) == 2) {
+        typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+        const u2 q = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+        v[0] = Elem<T>::to_f32(__builtin_bit_cast(T, (uint16_t)(q.x & 0xffffu)));
+        v[1] = Elem<T>::to_f32(__builtin_bit_cast(T, (uint16_t)(q.x >> 16)));
+        v[2] = Elem<T>::to_f32(__builtin_bit_cast(T, (uint16_t)(q.y & 0xffffu)));
+        v[3] = Elem<T>::to_f32(__builtin_bit_cast(T, (uint16_t)(q.y >> 16)));
+    } else {
+        static_assert(sizeof(T) == 1, "quad loads of 1/2/4-byte elements");
+        const uint32_t q = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            v[e] = Elem<T>::to_f32(__builtin_bit_cast(T, (uint8_t)((q >> (8 * e)) & 0xffu)));
+    }
+}
+
+// A workgroup stages the (TY + L - 1) x (TX + 2 MG) input tile from x0 - MG, MG = L/2 rounded up
+// to a multiple of 4 (whole 4-element quads; columns beyond the window are loaded, never read).
+// QUAD (block x extent and x origin multiples of 4, aligned base, <= 4-byte elements): each quad
+// is one 4/8/16-byte access at its start clamped to [0, nx - 4]; a quad wholly left / right of
+// the block then holds the edge element at position 0 / 3, broadcast when the quad enters the
+// ring (edge tiles only), which is the replicate clamping of the y / x passes. Otherwise
+// element by element at x clamped to the block.
+template <int L, typename TIn, bool QUAD>
 __global__ __launch_bounds__(256) void gauss_zyx_kernel(const TIn* __restrict__ in,
                                                         float* __restrict__ out, GaussZYX p,
                                                         int tiles_x, int tiles_y, int zseg) {
     constexpr int TY = kZYXTy, TX = kZYXTx, TH = TY + L - 1, TW = TX + L - 1, MID = L / 2;
-    constexpr int NE = TH * TW, NPT = (NE + 255) / 256;
+    constexpr int MG = (MID + 3) / 4 * 4;      // x margin of the staged tile (whole quads)
+    constexpr int TP = TX + 2 * MG, NQX = TP / 4;  // staged tile pitch (floats), quads per row
+    constexpr int NQ = TH * NQX, NPQ = (NQ + 255) / 256;  // quads, per thread
     constexpr int NYI = TW * (TY / 4), NXI = TY * (TX / 4);  // y / x pass items
     constexpr int NYP = (NYI + 255) / 256, NXP = (NXI + 255) / 256;
-    __shared__ float tile[NPT * 256];  // (rows past NE: the dummy writes of idle points)
+    __shared__ __attribute__((aligned(16))) float tile[NPQ * 256 * 4];  // rows past TH: dummies
     __shared__ float ybuf[TY * TW];
     const int tid = threadIdx.x;
     const int64_t nz = p.n[0], ny = p.n[1], nx = p.n[2];
@@ -388,117 +423,169 @@ __global__ __launch_bounds__(256) void gauss_zyx_kernel(const TIn* __restrict__ 
     const int64_t kz0 = (int64_t)seg * zseg, kz1 = kz0 + zseg < onz ? kz0 + zseg : onz;
     const int hy = (int)(ony - y0 < TY ? ony - y0 : TY);
     const int hx = (int)(onx - x0 < TX ? onx - x0 : TX);
-    const int64_t qy0 = p.o0[1] + y0 - MID, qx0 = p.o0[2] + x0 - MID;
+    const int64_t qy0 = p.o0[1] + y0 - MID, qx4 = p.o0[2] + x0 - MG;  // staged tile origin
     const int64_t plane = ny * nx;
     const uint32_t plane_bytes = (uint32_t)(plane * (int64_t)sizeof(TIn));
     const uint32_t oplane_bytes = (uint32_t)(ony * onx * 4);
-    int off[NPT];  // byte offset in the plane of each owned tile point (clamped, as the y / x
-                   // passes clamp)
-#pragma unroll
-    for (int k = 0; k < NPT; ++k) {
-        const int e = tid + 256 * k;
-        const int r = e / TW, c = e - r * TW;
-        int64_t qy = qy0 + r, qx = qx0 + c;
-        qy = qy < 0 ? 0 : (qy > ny - 1 ? ny - 1 : qy);
-        qx = qx < 0 ? 0 : (qx > nx - 1 ? nx - 1 : qx);
-        off[k] = e < NE ? (int)((qy * nx + qx) * (int64_t)sizeof(TIn)) : kZBad;
-    }
-    // x-pass items: output offset within the slice (kZBad for rows / quads outside the box);
-    // whole quads when the box width and the row pitch keep them inside and 16-byte aligned
+    // x-pass stores: whole quads when the box width and the row pitch keep them inside and
+    // 16-byte aligned
     const bool quads = (onx % 4 == 0) && (x0 % 4 == 0) && (((uintptr_t)out & 15) == 0);
-    for (int64_t o = blockIdx.y; o < p.outer; o += gridDim.y) {
-        const char* vol = reinterpret_cast<const char*>(in) + o * nz * plane * (int64_t)sizeof(TIn);
-        auto slice = [&](int64_t zq) {  // input slice zq, clamped (wave-uniform)
-            zq = zq < 0 ? 0 : (zq > nz - 1 ? nz - 1 : zq);
-            return z_rsrc(vol + zq * plane * (int64_t)sizeof(TIn), plane_bytes);
-        };
-        auto ld = [&](int64_t zq, float (&v)[NPT]) {
-            const zrsrc_t rs = slice(zq);
+    {
+        constexpr int NOFF = QUAD ? NPQ : 4 * NPQ;
+        int off[NOFF];  // byte offsets in the plane (rows clamped; x clamped per element)
+        // QUAD edge tiles: bit k of bl / br = quad k lies wholly left / right of the block
+        const bool edgex = qx4 < 0 || qx4 + TP > nx;  // block-uniform
+        int bl = 0, br = 0;
 #pragma unroll
-            for (int k = 0; k < NPT; ++k) v[k] = z_load<TIn>(rs, off[k]);
-        };
-        float ring[L][NPT], pre[NPT];
-        // window of the first output slice: position i = input slice o0 + kz0 + i - MID in slot
-        // i; position L - 1 arrives through pre
+        for (int k = 0; k < NPQ; ++k) {
+            const int q = tid + 256 * k;
+            const int r = q / NQX, cq = q - r * NQX;
+            int64_t qy = qy0 + r;
+            qy = qy < 0 ? 0 : (qy > ny - 1 ? ny - 1 : qy);
+            if constexpr (QUAD) {
+                int64_t xs = qx4 + 4 * cq;
+                bl |= xs < 0 ? 1 << k : 0;
+                br |= xs > nx - 4 ? 1 << k : 0;
+                xs = xs < 0 ? 0 : (xs > nx - 4 ? nx - 4 : xs);
+                off[k] = q < NQ ? (int)((qy * nx + xs) * (int64_t)sizeof(TIn)) : kZBad;
+            } else {
 #pragma unroll
-        for (int i = 0; i < L - 1; ++i) ld(p.o0[0] + kz0 + i - MID, ring[i]);
-        ld(p.o0[0] + kz0 + L - 1 - MID, pre);
-        char* obase = reinterpret_cast<char*>(out) + o * onz * ony * onx * 4;
-        for (int64_t kb = kz0; kb < kz1; kb += L) {
-            static_for<0, L>([&](auto PH_) {
-                constexpr int PH = decltype(PH_)::value;
-                // no early exit: the last block of L steps runs whole (an exit here put a
-                // vmcnt(0) drain on the loop path); steps past the segment store nothing
-                const int64_t kz = kb + PH;
-                // slot of window position i at this phase: (PH + i) % L; position L - 1 is new
-#pragma unroll
-                for (int k = 0; k < NPT; ++k) ring[(PH + L - 1) % L][k] = pre[k];
-                // next step's entering slice, unconditionally (clamped; unused past the segment)
-                ld(p.o0[0] + kz + 1 + MID, pre);
-#pragma unroll
-                for (int k = 0; k < NPT; ++k) {
-                    float sum = -0.0f;  // Iterator::sum::<f32> (kernel.rs:46, :66)
-#pragma unroll
-                    for (int i = 0; i < L; ++i) sum = sum + ring[(PH + i) % L][k] * p.w[0][i];
-                    tile[tid + 256 * k] = sum;
+                for (int e = 0; e < 4; ++e) {
+                    int64_t qx = qx4 + 4 * cq + e;
+                    qx = qx < 0 ? 0 : (qx > nx - 1 ? nx - 1 : qx);
+                    off[4 * k + e] = q < NQ ? (int)((qy * nx + qx) * (int64_t)sizeof(TIn)) : kZBad;
                 }
-                z_lds_barrier();
+            }
+        }
+        for (int64_t o = blockIdx.y; o < p.outer; o += gridDim.y) {
+            const char* vol =
+                reinterpret_cast<const char*>(in) + o * nz * plane * (int64_t)sizeof(TIn);
+            auto ld = [&](int64_t zq, float (&v)[NPQ][4]) {  // input slice zq (clamped)
+                zq = zq < 0 ? 0 : (zq > nz - 1 ? nz - 1 : zq);
+                const zrsrc_t rs = z_rsrc(vol + zq * plane * (int64_t)sizeof(TIn), plane_bytes);
 #pragma unroll
-                for (int ip = 0; ip < NYP; ++ip) {  // y pass, 4 rows per item
-                    const int item = tid + 256 * ip;
-                    if (NYI % 256 == 0 || item < NYI) {
-                        const int c = item % TW, r0 = (item / TW) * 4;
+                for (int k = 0; k < NPQ; ++k) {
+                    if constexpr (QUAD) {
+                        z_load4<TIn>(rs, off[k], v[k]);
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) v[k][e] = z_load<TIn>(rs, off[4 * k + e]);
+                    }
+                }
+            };
+            float ring[L][NPQ][4], pre[NPQ][4];
+            // window of the first output slice: position i = input slice o0 + kz0 + i - MID in
+            // slot i; position L - 1 arrives through pre
+            // edge quads of a QUAD march: the edge element broadcast (no memory instructions,
+            // applied where a slice enters the ring, a step after its load)
+            auto fix = [&](float (&v)[NPQ][4]) {
+                if constexpr (QUAD) {
+                    if (edgex) {
+#pragma unroll
+                        for (int k = 0; k < NPQ; ++k) {
+                            const bool l = (bl >> k) & 1, rr = (br >> k) & 1;
+#pragma unroll
+                            for (int e = 0; e < 4; ++e)
+                                v[k][e] = l ? v[k][0] : (rr ? v[k][3] : v[k][e]);
+                        }
+                    }
+                }
+            };
+#pragma unroll
+            for (int i = 0; i < L - 1; ++i) {
+                ld(p.o0[0] + kz0 + i - MID, ring[i]);
+                fix(ring[i]);
+            }
+            ld(p.o0[0] + kz0 + L - 1 - MID, pre);
+            char* obase = reinterpret_cast<char*>(out) + o * onz * ony * onx * 4;
+            for (int64_t kb = kz0; kb < kz1; kb += L) {
+                static_for<0, L>([&](auto PH_) {
+                    constexpr int PH = decltype(PH_)::value;
+                    // no early exit: the last block of L steps runs whole (an exit here put a
+                    // vmcnt(0) drain on the loop path); steps past the segment store nothing
+                    const int64_t kz = kb + PH;
+                    // slot of window position i at this phase: (PH + i) % L; L - 1 is new
+#pragma unroll
+                    for (int k = 0; k < NPQ; ++k)
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) ring[(PH + L - 1) % L][k][e] = pre[k][e];
+                    fix(ring[(PH + L - 1) % L]);
+                    // next step's entering slice, unconditionally (clamped; unused past the end)
+                    ld(p.o0[0] + kz + 1 + MID, pre);
+#pragma unroll
+                    for (int k = 0; k < NPQ; ++k) {
+                        float sv[4];
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            float sum = -0.0f;  // Iterator::sum::<f32> (kernel.rs:46, :66)
+#pragma unroll
+                            for (int i = 0; i < L; ++i)
+                                sum = sum + ring[(PH + i) % L][k][e] * p.w[0][i];
+                            sv[e] = sum;
+                        }
+                        *reinterpret_cast<float4*>(tile + 4 * (tid + 256 * k)) =
+                            make_float4(sv[0], sv[1], sv[2], sv[3]);
+                    }
+                    z_lds_barrier();
+#pragma unroll
+                    for (int ip = 0; ip < NYP; ++ip) {  // y pass, 4 rows per item
+                        const int item = tid + 256 * ip;
+                        if (NYI % 256 == 0 || item < NYI) {
+                            // column c of the TW window = staged column c + MG - MID
+                            const int c = item % TW, r0 = (item / TW) * 4;
+                            float v[4 + L - 1];
+#pragma unroll
+                            for (int j = 0; j < 4 + L - 1; ++j)
+                                v[j] = tile[(r0 + j) * TP + c + MG - MID];
+#pragma unroll
+                            for (int k = 0; k < 4; ++k) {
+                                float sum = -0.0f;
+#pragma unroll
+                                for (int i = 0; i < L; ++i) sum = sum + v[k + i] * p.w[1][i];
+                                ybuf[(r0 + k) * TW + c] = sum;
+                            }
+                        }
+                    }
+                    z_lds_barrier();
+                    const zrsrc_t ro = z_rsrc(obase + (kz < kz1 ? kz : 0) * ony * onx * 4,
+                                              kz < kz1 ? oplane_bytes : 0u);
+#pragma unroll
+                    for (int ip = 0; ip < NXP; ++ip) {  // x pass, 4 columns per item
+                        const int item = tid + 256 * ip;
+                        const int r = item / (TX / 4), c0 = (item % (TX / 4)) * 4;
+                        const bool live = (NXI % 256 == 0 || item < NXI) && r < hy;
                         float v[4 + L - 1];
 #pragma unroll
-                        for (int j = 0; j < 4 + L - 1; ++j) v[j] = tile[(r0 + j) * TW + c];
+                        for (int j = 0; j < 4 + L - 1; ++j)
+                            v[j] = ybuf[(live ? r : 0) * TW + c0 + j];
+                        float o4[4];
 #pragma unroll
                         for (int k = 0; k < 4; ++k) {
                             float sum = -0.0f;
 #pragma unroll
-                            for (int i = 0; i < L; ++i) sum = sum + v[k + i] * p.w[1][i];
-                            ybuf[(r0 + k) * TW + c] = sum;
+                            for (int i = 0; i < L; ++i) sum = sum + v[k + i] * p.w[2][i];
+                            o4[k] = sum;
+                        }
+                        const int ooff = (int)(((y0 + r) * onx + x0 + c0) * 4);
+                        if (quads) {
+                            typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+                            const u4 q = {__float_as_uint(o4[0]), __float_as_uint(o4[1]),
+                                          __float_as_uint(o4[2]), __float_as_uint(o4[3])};
+                            __builtin_amdgcn_raw_buffer_store_b128(
+                                q, ro, live && c0 < hx ? ooff : kZBad, 0, 2);
+                        } else {
+#pragma unroll
+                            for (int k = 0; k < 4; ++k)
+                                __builtin_amdgcn_raw_buffer_store_b32(
+                                    __float_as_uint(o4[k]), ro,
+                                    live && c0 + k < hx ? ooff + 4 * k : kZBad, 0, 2);
                         }
                     }
-                }
-                z_lds_barrier();
-                const zrsrc_t ro =
-                    z_rsrc(obase + (kz < kz1 ? kz : 0) * ony * onx * 4, kz < kz1 ? oplane_bytes : 0u);
-#pragma unroll
-                for (int ip = 0; ip < NXP; ++ip) {  // x pass, 4 columns per item
-                    const int item = tid + 256 * ip;
-                    const int r = item / (TX / 4), c0 = (item % (TX / 4)) * 4;
-                    const bool live = (NXI % 256 == 0 || item < NXI) && r < hy;
-                    float v[4 + L - 1];
-#pragma unroll
-                    for (int j = 0; j < 4 + L - 1; ++j)
-                        v[j] = ybuf[(live ? r : 0) * TW + c0 + j];
-                    float o4[4];
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        float sum = -0.0f;
-#pragma unroll
-                        for (int i = 0; i < L; ++i) sum = sum + v[k + i] * p.w[2][i];
-                        o4[k] = sum;
-                    }
-                    const int ooff = (int)(((y0 + r) * onx + x0 + c0) * 4);
-                    if (quads) {
-                        typedef unsigned int u4 __attribute__((ext_vector_type(4)));
-                        const u4 q = {__float_as_uint(o4[0]), __float_as_uint(o4[1]),
-                                      __float_as_uint(o4[2]), __float_as_uint(o4[3])};
-                        __builtin_amdgcn_raw_buffer_store_b128(
-                            q, ro, live && c0 < hx ? ooff : kZBad, 0, 2);
-                    } else {
-#pragma unroll
-                        for (int k = 0; k < 4; ++k)
-                            __builtin_amdgcn_raw_buffer_store_b32(
-                                __float_as_uint(o4[k]), ro,
-                                live && c0 + k < hx ? ooff + 4 * k : kZBad, 0, 2);
-                    }
-                }
-                // the next tile / ybuf writes follow this step's barriers (see gauss_yx_fast)
-            });
+                    // the next tile / ybuf writes follow this step's barriers
+                });
+            }
+            z_lds_barrier();  // the last step's reads of tile / ybuf before the next volume
         }
-        z_lds_barrier();  // the last step's reads of tile / ybuf before the next outer volume
     }
 }
 
@@ -529,8 +616,21 @@ static hipError_t launch_zyx_l(const void* in, int dtype_in, float* out, const G
     const dim3 grid((unsigned)gx, (unsigned)(outer < 65535 ? outer : 65535));
     hipError_t err = hipErrorInvalidValue;
     ZT_DISPATCH_DTYPE(dtype_in, T,
-        hipLaunchKernelGGL((gauss_zyx_kernel<L, T>), grid, dim3(256), 0, s,
-                           static_cast<const T*>(in), out, p, tiles_x, tiles_y, zseg);
+        // (quad instantiations for the common element types only: build time)
+        if constexpr (std::is_same_v<T, float> || std::is_same_v<T, uint16_t> ||
+                      std::is_same_v<T, uint8_t>) {
+            // quads need a 4-aligned x origin and extent and an aligned base
+            if (p.n[2] % 4 == 0 && p.o0[2] % 4 == 0 && p.n[2] >= 4 &&
+                (uintptr_t)in % (4 * sizeof(T)) == 0)
+                hipLaunchKernelGGL((gauss_zyx_kernel<L, T, true>), grid, dim3(256), 0, s,
+                                   static_cast<const T*>(in), out, p, tiles_x, tiles_y, zseg);
+            else
+                hipLaunchKernelGGL((gauss_zyx_kernel<L, T, false>), grid, dim3(256), 0, s,
+                                   static_cast<const T*>(in), out, p, tiles_x, tiles_y, zseg);
+        } else {
+            hipLaunchKernelGGL((gauss_zyx_kernel<L, T, false>), grid, dim3(256), 0, s,
+                               static_cast<const T*>(in), out, p, tiles_x, tiles_y, zseg);
+        }
         err = hipGetLastError())
     return err;
 }
