@@ -35,6 +35,10 @@ namespace zt {
 namespace {
 
 constexpr int kFTX = 64, kFTY = 8, kFTS = 4;  // tile width, height, timepoints per block
+#ifndef G4_KX2
+#define G4_KX2 5  // S2 outputs per item: 4 x 16 x ceil(68 / 5) = 896 items, one pass of 1024
+                  // threads (4 per item: 1088, a second pass for one wave)
+#endif
 #ifndef G4_STX
 #define G4_STX 4  // XCD super-tile of the tile walk: tiles along x
 #endif
@@ -50,7 +54,7 @@ struct G4FConfig {
     static constexpr int NT = 1024;  // one workgroup per CU, 4 waves per SIMD
     static constexpr int NE2 = E2X * E2Y, NPT = (NE2 + NT - 1) / NT;  // S1 points per thread per t
     static constexpr int PZ = ((E2X + 4 + 1) / 2) * 2;  // Z1 pitch (x-sum segments read past E2X)
-    static constexpr int KX2 = 4, NSX2 = (E1X + KX2 - 1) / KX2, NI2 = TS * E2Y * NSX2;
+    static constexpr int KX2 = G4_KX2, NSX2 = (E1X + KX2 - 1) / KX2, NI2 = TS * E2Y * NSX2;
     static constexpr int KY3 = 2, NSY3 = (E1Y + KY3 - 1) / KY3, NI3 = E1X * NSY3;
     static constexpr int KX4 = 8, NI4 = TS * E1Y * (TX / KX4);
     static constexpr int NI5 = TX * TY;

@@ -128,11 +128,18 @@ void c_strides(const int64_t* shape, int ndim, int64_t* strides) {
 }
 
 // Choose the z-march length for a fused launch: whole chunk depths when there is enough
-// parallelism, shorter segments for a single small block.
+// parallelism, shorter segments for a single small block. Segments are a free choice (windows
+// are clamped at the array, not the segment), so large launches march two chunk depths while
+// they keep >= 4096 workgroups (16 per CU): each segment re-fills its z-windows over 2r + 1
+// warm-up slices and pads its steps to a multiple of 2r + 1 (2048^3 r=4: 31.4 -> 30.6 ms;
+// 384- and 1024-slice segments measured slower, tools/timek.sh).
 int choose_zseg(int onz, int tiles, int radius, int chunk_depth) {
     const int target_wg = 1024;
     int zseg = chunk_depth > 0 ? std::min(chunk_depth, onz) : onz;
     if (zseg <= 0) zseg = 1;
+    if (chunk_depth > 0 && 2LL * chunk_depth <= onz &&
+        (int64_t)tiles * ((onz + 2 * chunk_depth - 1) / (2 * chunk_depth)) >= 4096)
+        zseg = 2 * chunk_depth;
     int64_t wg = (int64_t)tiles * ((onz + zseg - 1) / zseg);
     if (wg < target_wg && chunk_depth <= 0) {
         int nseg = (target_wg + tiles - 1) / std::max(tiles, 1);
