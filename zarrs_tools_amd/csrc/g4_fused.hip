@@ -39,6 +39,9 @@ constexpr int kFTX = 64, kFTY = 8, kFTS = 4;  // tile width, height, timepoints 
 #define G4_ABL 0  // tools/timeg4 ablations only (1: no leaving-slice loads, 2: no entering-slice
                   // loads, 8: no S3 / S5 v loads)
 #endif
+#ifndef G4_Q4
+#define G4_Q4 1  // quad loads in S1 where the geometry allows (see g4_fused_kernel)
+#endif
 #ifndef G4_KX2
 #define G4_KX2 5  // S2 outputs per item: 4 x 16 x ceil(68 / 5) = 896 items, one pass of 1024
                   // threads (4 per item: 1088, a second pass for one wave)
@@ -139,7 +142,12 @@ __device__ __forceinline__ void sfor(F&& f) {
     }
 }
 
-template <int R, typename TOut>
+// Q4: S1 reads 16-byte quads (4 consecutive x) instead of single elements: 4x fewer
+// vector-memory instructions for the stage-1 slices. Needs quads that never straddle the block
+// edge (x origin of the apron and the block width multiples of 4: r = 2 with aligned geometry);
+// waves [4t, 4t + 4) then hold timepoint t's quads, so each load's slice descriptor stays
+// wave-uniform.
+template <int R, typename TOut, bool Q4>
 __global__ __launch_bounds__(G4FConfig<R>::NT) void g4_fused_kernel(G4FParams p) {
     using C = G4FConfig<R>;
     constexpr int TX = C::TX, TY = C::TY, TS = C::TS, W = C::W, NT = C::NT, NPT = C::NPT;
@@ -216,18 +224,54 @@ __global__ __launch_bounds__(G4FConfig<R>::NT) void g4_fused_kernel(G4FParams p)
     };
     auto ldv = [&](int t, int z, int o) -> float { return ldb(slice(t, z), o); };
     const int zc_begin = zo_begin - R, zc_end = zo_end + R;  // stage-1 slices of this march
-    double zv[TS][NPT];
-    float pa[TS][NPT], ps[TS][NPT];
+    // element form: every thread NPT apron points of every timepoint
+    constexpr int TSE = Q4 ? 1 : TS, NPE = Q4 ? 1 : NPT;
+    double zv[TSE][NPE];
+    float pa[TSE][NPE], ps[TSE][NPE];
+    // quad form: timepoint tq (wave-uniform), NPQ quads of its apron per thread
+    constexpr int NQR = E2X / 4, NQT = E2Y * NQR, LPT = NT / TS;
+    constexpr int NPQ = Q4 ? (NQT + LPT - 1) / LPT : 1;
+    static_assert(!Q4 || (E2X % 4 == 0 && NT % (64 * TS) == 0), "quad S1 geometry");
+    const int tq = wave / (NT / 64 / TS), lq = tid - tq * LPT;
+    int offq[NPQ], z1q[NPQ];
+    double zq[NPQ][4];
+    float paq[NPQ][4], psq[NPQ][4];
+    auto ldq = [&](rsrc_t r, int o, float (&v)[4]) {
+        typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+        const u4 q = __builtin_amdgcn_raw_buffer_load_b128(r, o, 0, 0);
+        v[0] = __uint_as_float(q.x); v[1] = __uint_as_float(q.y);
+        v[2] = __uint_as_float(q.z); v[3] = __uint_as_float(q.w);
+    };
+    if constexpr (Q4) {
 #pragma unroll
-    for (int t = 0; t < TS; ++t)
+        for (int k = 0; k < NPQ; ++k) {
+            const int qi = lq + LPT * k, ey = qi / NQR, cq = qi - (qi / NQR) * NQR;
+            const int gy = y0 - 2 * R + ey, gx = x0 - 2 * R + 4 * cq;
+            offq[k] = (qi < NQT && gy >= 0 && gy < ny && gx >= 0 && gx < nx) ? (gy * nx + gx) * 4 : kBad;
+            z1q[k] = qi < NQT ? (tq * E2Y + ey) * PZ + 4 * cq : -1;
 #pragma unroll
-        for (int k = 0; k < NPT; ++k) {
-            double s = 0.0;
-            for (int z = zc_begin - 1 - R; z <= zc_begin - 1 + R; ++z) s += (double)ldv(t, z, off[k]);
-            zv[t][k] = s;
-            pa[t][k] = ldv(t, zc_begin + R, off[k]);
-            ps[t][k] = ldv(t, zc_begin - R - 1, off[k]);
+            for (int e = 0; e < 4; ++e) zq[k][e] = 0.0;
+            for (int z = zc_begin - 1 - R; z <= zc_begin - 1 + R; ++z) {
+                float v[4];
+                ldq(slice(tq, z), offq[k], v);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) zq[k][e] += (double)v[e];
+            }
+            ldq(slice(tq, zc_begin + R), offq[k], paq[k]);
+            ldq(slice(tq, zc_begin - R - 1), offq[k], psq[k]);
         }
+    } else {
+#pragma unroll
+        for (int t = 0; t < TS; ++t)
+#pragma unroll
+            for (int k = 0; k < NPT; ++k) {
+                double s = 0.0;
+                for (int z = zc_begin - 1 - R; z <= zc_begin - 1 + R; ++z) s += (double)ldv(t, z, off[k]);
+                zv[t][k] = s;
+                pa[t][k] = ldv(t, zc_begin + R, off[k]);
+                ps[t][k] = ldv(t, zc_begin - R - 1, off[k]);
+            }
+    }
 
     // ---- S3 item: column ex1 of the (a, b) apron, rows [KY3*sg, KY3*sg + KY3) --------------
     const int i3 = tid < C::NI3 ? tid : -1;
@@ -285,6 +329,27 @@ __global__ __launch_bounds__(G4FConfig<R>::NT) void g4_fused_kernel(G4FParams p)
         {
             const int zc = zc_begin + i, zo = zc - R;
             // S1: z-window update, Z1 writes, next step's entering / leaving slices
+            if constexpr (Q4) {
+#pragma unroll
+                for (int k = 0; k < NPQ; ++k) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        zq[k][e] = zq[k][e] + (double)paq[k][e];
+                        zq[k][e] = zq[k][e] - (double)psq[k][e];
+                    }
+                    if (z1q[k] >= 0) {
+                        double2* d = reinterpret_cast<double2*>(Z1 + z1q[k]);
+                        d[0] = make_double2(zq[k][0], zq[k][1]);
+                        d[1] = make_double2(zq[k][2], zq[k][3]);
+                    }
+                }
+                const rsrc_t ra = slice(tq, zc + 1 + R), rl = slice(tq, zc - R);
+#pragma unroll
+                for (int k = 0; k < NPQ; ++k) {
+                    ldq(ra, offq[k], paq[k]);
+                    ldq(rl, offq[k], psq[k]);
+                }
+            } else {
 #pragma unroll
             for (int t = 0; t < TS; ++t)
 #pragma unroll
@@ -304,6 +369,7 @@ __global__ __launch_bounds__(G4FConfig<R>::NT) void g4_fused_kernel(G4FParams p)
                     if constexpr (G4_ABL & 1) ps[t][k] = ps[t][k] * 0.998f;
                     else ps[t][k] = ldb(rl, off[k]);
                 }
+            }
             }
             lds_barrier();
             // S2: x-window sums of every apron row (f64)
@@ -469,9 +535,14 @@ hipError_t launch_fused4(G4FParams p, hipStream_t s) {
     nseg = (p.on[1] + p.zseg - 1) / p.zseg;
     const int64_t gx = tiles * nseg;
     if (gx > 0x7FFFFFFF) return hipErrorInvalidValue;
-    auto kern = g4_fused_kernel<R, TOut>;
+    // quad S1 (Q4) when no quad of the stage-1 apron straddles the block's x edges
+    const bool q4 = R == 2 && G4_Q4 && p.nx % 4 == 0 && p.o0[3] % 4 == 0 &&
+                    (uintptr_t)p.v % 16 == 0;
+    auto kern = q4 ? g4_fused_kernel<R, TOut, true> : g4_fused_kernel<R, TOut, false>;
     // > 64 KB of dynamic LDS needs the opt-in, once per device (a bit per device)
-    static std::atomic<uint64_t> attr{0};
+    // (one mask per kernel variant)
+    static std::atomic<uint64_t> attr_q[2] = {{0}, {0}};
+    std::atomic<uint64_t>& attr = attr_q[q4 ? 1 : 0];
     int dev = 0;
     if (hipError_t e = hipGetDevice(&dev)) return e;
     if (!(attr.load(std::memory_order_relaxed) & (1ull << (dev & 63)))) {
