@@ -17,6 +17,12 @@
 #ifndef GF_T3_TOP
 #define GF_T3_TOP 1
 #endif
+#ifndef GF_K4_R4
+#define GF_K4_R4 8
+#endif
+#ifndef GF_ORDER_R4
+#define GF_ORDER_R4 2
+#endif
 #ifndef GF_PRIO
 #define GF_PRIO 1  // s_setprio phase reordering (measured -4.5% at 2048^3 r=4 with the b128 Hx writes)
 #endif
@@ -511,7 +517,11 @@ struct GFConfig {
     static constexpr int PH = p2m4(E1X);  // Hx  (f64)    P12 writes rows, P3 reads columns
     static constexpr int PA = p2m4(E1X);  // Lab (float2) P3 writes, P4 reads rows
     static constexpr int PB = p2m4(TX);   // Hab (float2) P4 writes rows, P5 reads columns
-    static constexpr int K3 = GF_K3, K4 = GF_K4;
+    // r = 4 (the headline radius, 64 x 32 tiles): 8 outputs per P4 item and P4 issued ahead of
+    // P12 in C1 (each -2 % at 2048^3, tools/timek.sh); other radii keep the defaults (unmeasured)
+    static constexpr bool R4 = R == 4 && TY == 32 && NT == 1024;
+    static constexpr int K3 = GF_K3, K4 = R4 ? GF_K4_R4 : GF_K4;
+    static constexpr int ORDER = R4 ? GF_ORDER_R4 : GF_ORDER;
     static constexpr int K5 = TX * TY / NT;          // outputs per thread (ring width)
     static constexpr int S3 = (E1Y + K3 - 1) / K3;   // segments per column, P3
     static constexpr int S4 = TX / K4;               // segments per row, P4
@@ -1275,7 +1285,7 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
             // wave drops its priority as it completes a phase, so laggards catch up.
             if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(3);
             // C0: P3(i) + P5(i-1) (LDS and registers only)
-            if constexpr (GF_ORDER & 1) {
+            if constexpr (C::ORDER & 1) {
                 if (i > zc_begin) do_p5(tid, i - 1, std::integral_constant<int, (k + W - 1) % W>{});
                 if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(1);
                 do_p3(tid, i);
@@ -1309,12 +1319,12 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
 #endif
             stamp(6);
             if constexpr (GF_PRIO >= 2) __builtin_amdgcn_s_setprio(2);
-            if constexpr (GF_ORDER & 2) do_p4(tid);
+            if constexpr (C::ORDER & 2) do_p4(tid);
             do_p12(tid);
             load_p1(rs_in(ob + off_a, zb + 2 * R + 1), r_b);
             if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(1);
             stamp(5);
-            if constexpr (!(GF_ORDER & 2)) do_p4(tid);
+            if constexpr (!(C::ORDER & 2)) do_p4(tid);
             stamp(3);
             lds_barrier_abl<ABL>();
             ++zb;
