@@ -17,6 +17,9 @@ using namespace zt;
 #ifndef TK_TY
 #define TK_TY 32
 #endif
+#ifndef TK_R
+#define TK_R 4
+#endif
 #ifndef TK_NT
 #define TK_NT 1024
 #endif
@@ -45,10 +48,10 @@ int main(int argc, char** argv) {
     hipEvent_t a, b;
     CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
     std::vector<float> t;
-    CK((launch_fused_cfg<4, TK_TY, TK_NT, float, float, TK_ABL>(p, s)));
+    CK((launch_fused_cfg<TK_R, TK_TY, TK_NT, float, float, TK_ABL>(p, s)));
     for (int r = 0; r < 5; ++r) {
         CK(hipEventRecord(a, s));
-        CK((launch_fused_cfg<4, TK_TY, TK_NT, float, float, TK_ABL>(p, s)));
+        CK((launch_fused_cfg<TK_R, TK_TY, TK_NT, float, float, TK_ABL>(p, s)));
         CK(hipEventRecord(b, s));
         CK(hipEventSynchronize(b));
         float ms; CK(hipEventElapsedTime(&ms, a, b));

@@ -563,6 +563,8 @@ struct GFConfig {
     static constexpr int LDS_BYTES = OFF_DUMMY + 256;
     // item -> thread placement: heavy phases on different waves (see C0 / C1)
     static constexpr int T3 = GF_T3_TOP ? NT - N3 : 0;  // first thread of the P3 items
+    // (the bottom placement is not maintained: its P3 loads disagree with GF_DIRECT's item map)
+    static_assert(GF_T3_TOP || !GF_DIRECT, "GF_T3_TOP=0 needs GF_DIRECT=0");
     static_assert(TX * TY % NT == 0, "tile must divide evenly over the threads");
     static_assert(TY % K5 == 0, "ring segment must divide the tile height");
     static_assert(TX % K4 == 0, "P4 segment must divide the tile width");
