@@ -77,6 +77,21 @@ def test_all_output_types(dout):
     assert np.array_equal(out.view(np.uint8), want.view(np.uint8))
 
 
+# Quad staging of the fused march (gauss_zyx_kernel<.., QUAD>): x extent a multiple of 4, several
+# x tiles with edge quads on both sides, 1/2/4-byte inputs, the 128-VGPR form (L = 7) and the
+# widest margin (L = 13).
+@pytest.mark.parametrize("din", ["float32", "uint16", "uint8"])
+@pytest.mark.parametrize("half", [3, 6])
+def test_fused_zyx_quad_staging_bit_exact(din, half):
+    rng = np.random.default_rng(7 + half)
+    v32 = (rng.random((9, 37, 264), dtype=np.float32) * 250).astype(np.float32)
+    v = O.cast_from_f32(v32, din)
+    chunk = (9, 37, 264)
+    ref = O.gaussian_apply(O.cast_to_f32(v, din), chunk, [1.0, 1.3, 0.9], [half] * 3)
+    out = gpu_gaussian(v, din, "float32", chunk, [1.0, 1.3, 0.9], [half] * 3)
+    assert np.array_equal(out, ref)
+
+
 # The fused z/y/x march (gaussian.hip gauss_zyx_kernel): one tap length L on the last three
 # axes, L in 3..13; several tiles, z segments and chunk-region offsets.
 @pytest.mark.parametrize("shape,chunk,sigma,half", [

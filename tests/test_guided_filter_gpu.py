@@ -297,6 +297,18 @@ def test_guided4d_fused_vs_oracle_small_eps(shape, chunk, r):
     assert rel_err(gpu_apply_chunked(v, "float32", "float32", chunk, 0.5, r), ref) <= FLOAT_TOL
 
 
+# quad stage-1 loads (g4_fused_kernel<.., Q4>): r = 2, x extent a multiple of 4, several x tiles
+# (the last one partial), fewer than 4 timepoints (the waves of timepoint 3 read zero-record
+# descriptors), partial y tiles
+@pytest.mark.parametrize("shape", [(3, 20, 21, 136), (4, 11, 9, 200), (2, 9, 40, 68)])
+def test_guided4d_fused_quad_loads_vs_oracle(shape):
+    rng = np.random.default_rng(sum(shape))
+    v = (rng.random(shape, dtype=np.float32) * 300).astype(np.float32)
+    chunk = (shape[0], 8, 8, 64)
+    ref = O.guided_filter_apply(v, chunk, 0.5, 2, nthreads=8)
+    assert rel_err(gpu_apply(v, "float32", "float32", chunk, 0.5, 2), ref) <= FLOAT_TOL
+
+
 @pytest.mark.parametrize("din,dout", [("uint16", "float32"), ("float32", "uint8"),
                                       ("float64", "float16")])
 def test_guided4d_fused_element_types(din, dout):
