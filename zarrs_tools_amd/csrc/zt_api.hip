@@ -132,14 +132,24 @@ void c_strides(const int64_t* shape, int ndim, int64_t* strides) {
 // are clamped at the array, not the segment), so large launches march two chunk depths while
 // they keep >= 4096 workgroups (16 per CU): each segment re-fills its z-windows over 2r + 1
 // warm-up slices and pads its steps to a multiple of 2r + 1 (2048^3 r=4: 31.4 -> 30.6 ms;
-// 384- and 1024-slice segments measured slower, tools/timek.sh).
+// 384- and 1024-slice segments measured slower, tools/timek.sh; profiles/r02_ab_harness.txt).
 int choose_zseg(int onz, int tiles, int radius, int chunk_depth) {
     const int target_wg = 1024;
     int zseg = chunk_depth > 0 ? std::min(chunk_depth, onz) : onz;
     if (zseg <= 0) zseg = 1;
-    if (chunk_depth > 0 && 2LL * chunk_depth <= onz &&
-        (int64_t)tiles * ((onz + 2 * chunk_depth - 1) / (2 * chunk_depth)) >= 4096)
+    if (chunk_depth > 0 && radius <= 2) {
+        // short windows (5-slice warm-up): up to 4 chunk depths while >= 512 workgroups (2 per CU)
+        // remain (1024^3 r=2: 3.46 -> 3.33 ms for one 1024-slice segment per tile)
+        for (int m = 4; m >= 2; m /= 2)
+            if ((int64_t)m * chunk_depth <= onz &&
+                (int64_t)tiles * ((onz + m * chunk_depth - 1) / (m * chunk_depth)) >= 512) {
+                zseg = m * chunk_depth;
+                break;
+            }
+    } else if (chunk_depth > 0 && 2LL * chunk_depth <= onz &&
+               (int64_t)tiles * ((onz + 2 * chunk_depth - 1) / (2 * chunk_depth)) >= 4096) {
         zseg = 2 * chunk_depth;
+    }
     int64_t wg = (int64_t)tiles * ((onz + zseg - 1) / zseg);
     if (wg < target_wg && chunk_depth <= 0) {
         int nseg = (target_wg + tiles - 1) / std::max(tiles, 1);
