@@ -83,14 +83,28 @@ def maybe_launch(args) -> None:
     sys.exit(subprocess.call(cmd, env=env))
 
 
+def _affinity_count():
+    try:
+        return len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return None
+
+
 def cpu_baseline(gshape, radius: int, nchunks: int = 0):
     """Reference algorithm (C restatement of guided_filter.rs, oracle/) on a bounded sample of
     the same workload: chunks of the same synthetic volume, 256^3 chunks, each with its 2r halo,
-    all host threads (rayon default), faithful incl. the dead 4th SAT. The default sample, 6
+    every CPU of this process's affinity (rayon's default) capped at OMP_NUM_THREADS (the CPU
+    share a GPU box grants), faithful incl. the dead 4th SAT. The default sample, 6
     chunks per thread, is about 15 s of CPU work at 0.4 GiB/s."""
     from oracle import oracle as O
-    ncpu = os.cpu_count() or 1
-    threads = max(1, min(16, ncpu))  # the GPU box grants a 16-CPU share
+    ncpu = os.cpu_count() or 1  # every CPU of the machine (nproc-like)
+    try:  # the CPUs this process may run on (the GPU box grants a share of the machine)
+        threads = max(1, len(os.sched_getaffinity(0)))
+    except (AttributeError, OSError):
+        threads = ncpu
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:  # the share the box's scheduler grants (16 there)
+        threads = min(threads, int(omp))
     nchunks = nchunks or 6 * threads
     grid = [-(-g // CHUNK) for g in gshape]
     coords = [((i * 3) % grid[0], (i * 5 + 1) % grid[1], (i * 7 + 2) % grid[2])
@@ -98,9 +112,12 @@ def cpu_baseline(gshape, radius: int, nchunks: int = 0):
     secs, vox = O.time_guided_filter_chunks(gshape, (CHUNK,) * 3, coords, EPS, radius, threads)
     gibs = vox * 4 / 2 ** 30 / secs
     return {"value": round(gibs, 5), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "host_cpus": ncpu, "affinity_cpus": _affinity_count(),
             "sample": f"{nchunks} chunks of 256^3 (r={radius}, 2r halo) of the same "
                       f"{'x'.join(map(str, gshape))} synthetic volume, {secs:.2f} s wall on "
-                      f"{threads} threads; C restatement of guided_filter.rs "
+                      f"{threads} threads (host: {ncpu} CPUs, {_affinity_count()} in this "
+                      f"process's affinity, OMP_NUM_THREADS={omp or 'unset'}); "
+                      f"C restatement of guided_filter.rs "
                       f"(oracle/zt_oracle.c, faithful incl. dead SAT)"}
 
 

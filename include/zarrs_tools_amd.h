@@ -3,8 +3,10 @@
  *
  * This is the drop-in boundary for the reference's per-chunk filter apply (LDeakin/zarrs_tools
  * 0.7.2, Rust). A Rust host would bind these symbols through a thin `extern "C"` FFI
- * (INTEGRATION.md shows the binding); in this repo the host side above the ABI is C++ (the
- * zarrs_filter / zarrs_ome drivers in zarrs_tools_amd/csrc/host) and Python (ctypes, tests/bench).
+ * (INTEGRATION.md shows the binding). In this repo the host side above the ABI is Python over
+ * ctypes: the zarrs_filter / zarrs_ome drivers (zarrs_tools_amd/zarrs_filter.py, zarrs_ome.py),
+ * the tests and the bench; zarrs_tools_amd/csrc/host holds the C++ Zarr V3 store and the
+ * overlapped store -> store pipeline behind the zt_store_* entry points.
  *
  * Conventions
  *  - Plain pointers and sizes only. Array buffers are DEVICE pointers (hipMalloc / torch CUDA
@@ -198,6 +200,13 @@ int zt_synth_u16(zt_ctx* ctx, uint16_t* out, const int64_t* shape, int ndim,
 int zt_synth_box(zt_ctx* ctx, int kind, void* out, const int64_t* start, const int64_t* shape,
                  const int64_t* global_shape, int ndim, uint64_t seed);
 
+/* Reencode::apply_chunk_convert (src/filter/filters/reencode.rs:58-77): out[i] = in[i].as_() for
+ * n contiguous elements of any of the 13 types to any other (num-traits AsPrimitive, half 2.6.0:
+ * half types through f32, float -> int saturating with NaN -> 0, int -> int wrapping). Used by
+ * zarrs_ome's level 0 with --data-type (zarrs_ome.rs:355-363). */
+int zt_reencode_cast(zt_ctx* ctx, int dtype_in, const void* in, int dtype_out, void* out,
+                     int64_t n);
+
 
 /* ---- Gaussian (src/filter/filters/gaussian.rs; src/filter/kernel.rs) ----------------------- */
 
@@ -259,6 +268,14 @@ typedef struct zt_progress {
 } zt_progress;
 typedef void (*zt_progress_fn)(const zt_progress* progress, void* user);
 void zt_store_set_progress_callback(zt_progress_fn fn, void* user);
+
+/* --chunk-limit (zarrs_ome.rs:136-141; GuidedFilter::apply's chunk_limit, guided_filter.rs:
+ * 251-258): the store filters called afterwards FROM THIS THREAD hold at most `max_chunks` chunks
+ * in flight (decoded input rows + output rows being computed or encoded) and use at most that many
+ * host worker threads; the pipeline never goes below one input slab and one output row without
+ * overlap (a chunk row is its unit of device work). 0 (the default) = bounded by memory only.
+ * Replaces the reference's per-filter `chunk_limit` argument. */
+int zt_store_set_chunk_limit(int64_t max_chunks);
 
 /* flags for the store filters */
 #define ZT_STORE_ERASE_OUTPUT_METADATA 1 /* remove OUT/zarr.json first ("not finished" marker,

@@ -279,3 +279,125 @@ def test_store_step_split_over_processes_equals_one_process(tmp_path):
     gf = O.guided_filter_apply(v, chunk, 2500.0, 2, nthreads=8)
     want = O.downsample(gf, "float32", (1, 2, 2, 2), "float32")
     assert rel_err(S.read_array(tmp_path / "one.zarr"), want) <= FLOAT_TOL
+
+
+@pytest.mark.parametrize("gpus,mode", [(2, "mean"), (4, "mean"), (3, "discrete"),
+                                       (2, "gaussian")])
+def test_zarrs_ome_gpus_split_equals_one_process(tmp_path, gpus, mode):
+    """zarrs_ome --gpus N (rehearsed with every process on device 0): octant-owned levels with
+    host assembly of boundary chunks (mean / mode), or every level split by chunk rows
+    (--gaussian-sigma), give the one-process levels, level metadata and group metadata bit for
+    bit."""
+    shape, chunk = (64, 48, 80), (16, 16, 16)
+    u = O.synth_u16(shape)
+    S.create_array(tmp_path / "in.zarr", "uint16", shape, chunk)
+    S.write_array(tmp_path / "in.zarr", u)
+    kw = {"discrete": mode == "discrete"}
+    if mode == "gaussian":
+        kw.update(gaussian_sigma=[1.0, 1.0, 1.0], gaussian_kernel_half_size=[2, 2, 2])
+    a = ZO.run(str(tmp_path / "in.zarr"), str(tmp_path / "one"), log=lambda *x: None, **kw)
+    b = ZO.run(str(tmp_path / "in.zarr"), str(tmp_path / "many"), log=lambda *x: None,
+               gpus=gpus, gpu_devices=[0] * gpus, **kw)
+    if mode != "gaussian":
+        assert b["stats"][0]["processes"] == gpus and b["stats"][0]["assembled_chunks"] > 0
+    assert a["levels"] == b["levels"] >= 5
+    for lvl in range(a["levels"] + 1):
+        pa, pb = tmp_path / "one" / str(lvl), tmp_path / "many" / str(lvl)
+        assert not os.path.exists(pb / ZO.PENDING)
+        assert np.array_equal(S.read_array(pa), S.read_array(pb)), lvl
+        assert S.open_array(pa).metadata == S.open_array(pb).metadata
+    with open(tmp_path / "one" / "zarr.json") as f, open(tmp_path / "many" / "zarr.json") as g:
+        assert json.load(f) == json.load(g)
+
+
+def _rust_as(x, dt):
+    """Rust `as` from float to an integer type: NaN -> 0, truncation, saturation."""
+    info = np.iinfo(dt)
+    y = np.nan_to_num(np.trunc(x.astype(np.float64)), nan=0.0, posinf=info.max, neginf=info.min)
+    return np.clip(y, info.min, info.max).astype(dt)
+
+
+def test_zarrs_ome_level0_data_type_reencodes_with_as_casts(tmp_path):
+    """zarrs_ome -d: level 0 is the input converted with Rust `as` (Reencode, reencode.rs:58-77,
+    zarrs_ome.rs:355-363) and the pyramid is built from it."""
+    shape, chunk = (20, 24, 28), (8, 8, 8)
+    v = (O.synth_step_noise_f32(shape) - 100.0) * np.float32(0.6)  # below 0 and above 255
+    v[0, 0, :3] = [np.nan, np.inf, -np.inf]
+    S.create_array(tmp_path / "in.zarr", "float32", shape, chunk)
+    S.write_array(tmp_path / "in.zarr", v)
+    assert ZO.main([str(tmp_path / "in.zarr"), str(tmp_path / "ome"), "--max-levels", "2",
+                    "-d", "uint8"]) == 0
+    l0 = S.read_array(tmp_path / "ome" / "0")
+    np.testing.assert_array_equal(l0, _rust_as(v, np.uint8))
+    assert json.load(open(tmp_path / "ome" / "0" / "zarr.json"))["data_type"] == "uint8"
+    np.testing.assert_array_equal(S.read_array(tmp_path / "ome" / "1"),
+                                  O.downsample(l0, "uint8", (2, 2, 2), "uint8"))
+    # u16 -> f32 -> i16: exact values, then saturating truncation
+    S.create_array(tmp_path / "u.zarr", "uint16", shape, chunk)
+    u = O.synth_u16(shape)
+    S.write_array(tmp_path / "u.zarr", u)
+    assert ZO.main([str(tmp_path / "u.zarr"), str(tmp_path / "ome2"), "--max-levels", "1",
+                    "-d", "float32"]) == 0
+    np.testing.assert_array_equal(S.read_array(tmp_path / "ome2" / "0"), u.astype(np.float32))
+
+
+def test_reencode_cast_matrix_matches_rust_as():
+    """zt_reencode_cast over integer / float pairs whose Rust `as` numpy restates exactly."""
+    import torch
+    from zarrs_tools_amd import filter as F
+    rng = np.random.default_rng(3)
+    f = (rng.standard_normal(4096) * 300.0).astype(np.float32)
+    f[:4] = [np.nan, np.inf, -np.inf, -0.0]
+    i64 = rng.integers(-2 ** 40, 2 ** 40, 4096, dtype=np.int64)
+    dev = torch.device("cuda", 0)
+    for dt in (np.int8, np.int16, np.int32, np.uint8, np.uint16, np.uint32):
+        got = F.reencode_cast(torch.from_numpy(f).to(dev), np.dtype(dt).name).cpu().numpy()
+        np.testing.assert_array_equal(got, _rust_as(f, dt))
+        got = F.reencode_cast(torch.from_numpy(i64).to(dev), np.dtype(dt).name).cpu().numpy()
+        np.testing.assert_array_equal(got, i64.astype(dt))  # integer `as`: wrapping
+    got = F.reencode_cast(torch.from_numpy(i64).to(dev), "float32").cpu().numpy()
+    np.testing.assert_array_equal(got, i64.astype(np.float32))
+    got = F.reencode_cast(torch.from_numpy(f).to(dev), "float64").cpu().numpy()
+    np.testing.assert_array_equal(got, f.astype(np.float64))
+    got = F.reencode_cast(torch.from_numpy(f).to(dev), "float16").cpu().numpy()
+    np.testing.assert_array_equal(got.view(np.uint16), f.astype(np.float16).view(np.uint16))
+
+
+def test_device_chain_failure_leaves_no_finished_output(tmp_path, monkeypatch):
+    """A failing step of a device-resident chain leaves the chain output without zarr.json
+    (zarrs_filter.rs:297-313: metadata only once the filter has finished)."""
+    from zarrs_tools_amd import filter as F
+    shape, chunk = (32, 32, 32), (16, 16, 16)
+    S.create_array(tmp_path / "in.zarr", "float32", shape, chunk)
+    S.write_synth(tmp_path / "in.zarr")
+
+    def boom(*a, **k):
+        raise RuntimeError("injected failure")
+    monkeypatch.setattr(F.Gaussian, "apply", boom)
+    steps = [{"filter": "guided_filter", "input": str(tmp_path / "in.zarr"), "output": "$g",
+              "epsilon": 2500.0, "radius": 2},
+             {"filter": "gaussian", "output": str(tmp_path / "out.zarr"), "sigma": [1.0] * 3,
+              "kernel_half_size": [2] * 3}]
+    with pytest.raises(RuntimeError, match="injected"):
+        ZF.run(steps, tmp=str(tmp_path), log=lambda *a: None)
+    assert not os.path.exists(tmp_path / "out.zarr" / "zarr.json")
+
+
+def test_chunk_limit_bounds_chunks_in_flight(tmp_path):
+    """--chunk-limit caps the chunks held in flight and the host threads (guided_filter.rs:
+    251-258), down to one slab and one output row; the output is unchanged."""
+    shape, chunk = (64, 32, 32), (8, 16, 16)  # 4 chunks per row, 8 chunk rows
+    S.create_array(tmp_path / "in.zarr", "float32", shape, chunk)
+    S.write_synth(tmp_path / "in.zarr")
+    free = S.guided_filter(tmp_path / "in.zarr", tmp_path / "a.zarr", 2500.0, 2)
+    lim = S.guided_filter(tmp_path / "in.zarr", tmp_path / "b.zarr", 2500.0, 2, chunk_limit=20)
+    one = S.guided_filter(tmp_path / "in.zarr", tmp_path / "c.zarr", 2500.0, 2, chunk_limit=1)
+    # a slab needs 3 input rows (r=2 halo over 8-plane rows): 5 decoded rows + 2 output rows
+    # free; within 20 chunks 3 rows + 2 output rows; the floor is 3 rows + 1 output row
+    assert free["rows_in_flight"] * 4 + 8 > 20
+    assert (lim["rows_in_flight"], lim["double_buffered"]) == (3, 1)
+    assert lim["threads"] <= 20 and one["threads"] == 1
+    assert (one["rows_in_flight"], one["double_buffered"]) == (3, 0)
+    a = S.read_array(tmp_path / "a.zarr")
+    assert np.array_equal(a, S.read_array(tmp_path / "b.zarr"))
+    assert np.array_equal(a, S.read_array(tmp_path / "c.zarr"))

@@ -1,0 +1,61 @@
+"""CPU, multi-process: the orchestration of `zarrs_ome --gpus N` (zarrs_ome.run_octants). Each of
+N spawned processes owns a factor^L-aligned box of level 0 (shard.octant_assignment), computes its
+levels, writes the output chunks inside its box and hands the pieces of boundary-crossing chunks
+to the parent, which assembles and writes them. Here the per-level compute of
+each process is the oracle's downsample (test-only stand-in for the device kernel; the GPU test
+test_cli_gpu.py::test_zarrs_ome_gpus_split_equals_one_process runs the HIP path); the partition,
+the chunk writes, the host assembly and the pending-metadata protocol are the product code."""
+import json
+import os
+import shutil
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from zarrs_tools_amd import shard
+from zarrs_tools_amd import store as S
+from zarrs_tools_amd import zarrs_ome as ZO
+
+
+def _level_u16_2x(x):
+    """One 2x2x2 mean level of a uint16 box (downsample.rs:72-97), the oracle's restatement."""
+    return O.downsample(np.asarray(x), "uint16", (2, 2, 2), "uint16")
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_octant_processes_assemble_the_global_pyramid(tmp_path, world):
+    shape, chunk, factor = (64, 48, 80), (16, 16, 16), (2, 2, 2)
+    u = O.synth_u16(shape)
+    S.create_array(tmp_path / "in.zarr", "uint16", shape, chunk)
+    S.write_array(tmp_path / "in.zarr", u)
+    root = tmp_path / "ome"
+    os.makedirs(root)
+    shutil.copytree(tmp_path / "in.zarr", root / "0")
+    level_shapes = shard.pyramid_level_shapes(shape, factor, 10)
+    L = shard.octant_assignment(0, world, shape, factor, len(level_shapes)).local_levels
+    assert L >= 2
+    ZO.prepare_octant_levels(str(root), level_shapes, L)
+    done, st = ZO.run_octants(str(root), shape, factor, len(level_shapes), False, world,
+                              devices=[0] * world, log=lambda *a: None,
+                              compute=_level_u16_2x)
+    assert done == L
+    assert st["assembled_chunks"] > 0  # the upper levels cross box boundaries
+    want = u
+    for k in range(1, L + 1):
+        want = _level_u16_2x(want)
+        # not finished yet: no zarr.json until the parent publishes the level
+        assert not os.path.exists(root / str(k) / "zarr.json")
+        assert os.path.exists(root / str(k) / ZO.PENDING)
+        np.testing.assert_array_equal(S.read_array(root / str(k)), want)
+        ZO._publish_metadata(str(root / str(k)))
+        m = json.load(open(root / str(k) / "zarr.json"))
+        assert m["shape"] == list(level_shapes[k - 1])
+    # the scratch directory of the pieces is gone
+    assert not [p for p in os.listdir(root) if p.startswith(".zt_octants_")]
+
+
+def test_box_chunks_inner_box_and_touched_chunks():
+    lo, hi, i0, i1 = ZO._box_chunks((8, 0), (24, 40), (16, 16), (32, 40))
+    assert (lo, hi) == ([0, 0], [2, 3])
+    assert (i0, i1) == ([16, 0], [32, 40])  # the array end counts as a chunk boundary

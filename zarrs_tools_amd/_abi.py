@@ -164,6 +164,7 @@ def lib() -> ctypes.CDLL:
         "zt_synth_step_noise_f32": ([vp, vp, i64p, c_int, i64p, ctypes.c_int64, ctypes.c_uint64],
                                     c_int),
         "zt_synth_u16": ([vp, vp, i64p, c_int, i64p, ctypes.c_int64, ctypes.c_uint64], c_int),
+        "zt_reencode_cast": ([vp, c_int, vp, c_int, vp, ctypes.c_int64], c_int),
         "zt_synth_box": ([vp, c_int, vp, i64p, i64p, i64p, c_int, ctypes.c_uint64], c_int),
         # store -> store path (host storage)
         "zt_store_array_info": ([ctypes.c_char_p, ctypes.POINTER(c_int), ctypes.POINTER(c_int),
@@ -175,6 +176,7 @@ def lib() -> ctypes.CDLL:
         "zt_store_create_output_like": ([ctypes.c_char_p, ctypes.c_char_p, c_int,
                                          ctypes.c_char_p], c_int),
         "zt_store_set_progress_callback": ([PROGRESS_FN, vp], None),
+        "zt_store_set_chunk_limit": ([ctypes.c_int64], ctypes.c_int),
         "zt_store_read_subset": ([ctypes.c_char_p, i64p, i64p, vp, c_int], c_int),
         "zt_store_write_subset": ([ctypes.c_char_p, i64p, i64p, vp, c_int], c_int),
         "zt_store_write_synth": ([ctypes.c_char_p, c_int, ctypes.c_uint64, c_int], c_int),

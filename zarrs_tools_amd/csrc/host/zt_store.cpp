@@ -472,6 +472,18 @@ int report(const std::exception& e) {
 // of the available host RAM and 80 % of the free device memory, down to one row without overlap,
 // and the reference's error is returned when not even that fits. ZT_STORE_HOST_MEMORY /
 // ZT_STORE_DEVICE_MEMORY (bytes) override the available amounts (tests, co-tenant limits).
+// One unsigned number from a cgroup file; false when absent or "max" (no limit).
+bool read_cgroup_u64(const char* path, uint64_t& v) {
+    FILE* f = std::fopen(path, "r");
+    if (!f) return false;
+    char buf[64] = {0};
+    const bool got = std::fgets(buf, sizeof buf, f) != nullptr;
+    std::fclose(f);
+    if (!got || buf[0] < '0' || buf[0] > '9') return false;
+    v = std::strtoull(buf, nullptr, 10);
+    return true;
+}
+
 uint64_t host_available_bytes() {
     if (const char* e = std::getenv("ZT_STORE_HOST_MEMORY")) return std::strtoull(e, nullptr, 10);
     FILE* f = std::fopen("/proc/meminfo", "r");
@@ -482,8 +494,22 @@ uint64_t host_available_bytes() {
             if (std::sscanf(line, "MemAvailable: %lu kB", (unsigned long*)&kb) == 1) break;
         std::fclose(f);
     }
-    return kb ? kb * 1024 : (uint64_t)16 << 30;
+    uint64_t avail = kb ? kb * 1024 : (uint64_t)16 << 30;
+    // Inside a memory-limited cgroup MemAvailable describes the whole machine: cap it at the
+    // cgroup's limit minus its usage (v2: memory.max / memory.current, v1: limit / usage).
+    uint64_t lim = 0, use = 0;
+    if ((read_cgroup_u64("/sys/fs/cgroup/memory.max", lim) &&
+         read_cgroup_u64("/sys/fs/cgroup/memory.current", use)) ||
+        (read_cgroup_u64("/sys/fs/cgroup/memory/memory.limit_in_bytes", lim) &&
+         read_cgroup_u64("/sys/fs/cgroup/memory/memory.usage_in_bytes", use))) {
+        if (lim < ((uint64_t)1 << 60)) avail = std::min(avail, lim > use ? lim - use : 0);
+    }
+    return avail;
 }
+
+// --chunk-limit (zarrs_ome.rs:136-141, guided_filter.rs:251-258): the reference processes at
+// most this many chunks concurrently. Per calling thread; 0 = bounded by memory only.
+thread_local int64_t g_chunk_limit = 0;
 
 uint64_t device_available_bytes() {
     if (const char* e = std::getenv("ZT_STORE_DEVICE_MEMORY")) return std::strtoull(e, nullptr, 10);
@@ -554,6 +580,20 @@ void run_pipeline(const Array& in, const Array& out, int device, int64_t row_beg
         else if (NB > 1) NB = 1;
         else throw zt::zarr::Error(ZT_ERR_OUT_OF_MEMORY, kNotEnoughMemory);
     }
+    // --chunk-limit: the chunks held in flight (decoded input rows + output rows being computed
+    // or encoded) stay within the limit, down to the pipeline's unit of one slab and one output
+    // row without overlap (a chunk row is the device's unit of work)
+    const int64_t in_row_chunks = (int64_t)chunks_in_rows(in, 0, 1).size();
+    const int64_t out_row_chunks = (int64_t)chunks_in_rows(out, 0, 1).size();
+    int threads = resolve_threads(nthreads);
+    if (g_chunk_limit > 0) {
+        while (NR * in_row_chunks + NB * out_row_chunks > g_chunk_limit) {
+            if (NR > max_rows_per) --NR;
+            else if (NB > 1) NB = 1;
+            else break;
+        }
+        threads = (int)std::max<int64_t>(1, std::min<int64_t>(threads, g_chunk_limit));
+    }
 
     if (hipSetDevice(device) != hipSuccess)
         throw zt::zarr::Error(ZT_ERR_DEVICE, "hipSetDevice failed");
@@ -591,7 +631,7 @@ void run_pipeline(const Array& in, const Array& out, int device, int64_t row_beg
         dout[s].alloc((size_t)out_cz * out_pb);
     }
 
-    Pool pool(resolve_threads(nthreads));
+    Pool pool(threads);
     std::vector<Group> dec_group(NR);
     Group enc_group[2];
     std::vector<int64_t> ring_row(NR, -1);
@@ -1189,6 +1229,12 @@ void zt_store_set_progress_callback(zt_progress_fn fn, void* user) {
     std::lock_guard<std::mutex> lk(g_progress_mu);
     g_progress_fn = fn;
     g_progress_user = user;
+}
+
+int zt_store_set_chunk_limit(int64_t max_chunks) {
+    if (max_chunks < 0) return zt::set_last_error(ZT_ERR_INVALID_PARAMETERS, "chunk limit must be >= 0");
+    g_chunk_limit = max_chunks;
+    return ZT_OK;
 }
 
 int zt_store_codec_available(const char* name) {

@@ -626,6 +626,10 @@ void copy_box(const uint8_t* src, const int64_t* ss, uint8_t* dst, const int64_t
 Array Array::open(const std::string& path) {
     bool exists = false;
     std::string text = read_file(path + "/zarr.json", &exists);
+    // An array being written by several processes keeps its metadata under a name Zarr readers
+    // do not see until the writer publishes it (renames it to zarr.json) once every chunk is in:
+    // the reference's store_metadata-after-the-chunks order (zarrs_ome.rs:729), across processes.
+    if (!exists) text = read_file(path + "/" + kPendingMetadata, &exists);
     if (!exists) raise(ZT_ERR_STORAGE, "no Zarr V3 array at " + path + " (zarr.json missing)");
     json::Value m;
     try {

@@ -28,6 +28,10 @@ struct Error : std::runtime_error {
 };
 
 int dtype_from_name(const std::string& name);   // zt_dtype, or -1
+
+// Metadata of an array that is not finished yet (written by several processes); Array::open
+// falls back to it when zarr.json is absent.
+constexpr const char* kPendingMetadata = ".zt_pending.json";
 const char* dtype_name(int dtype);
 size_t dtype_size(int dtype);
 

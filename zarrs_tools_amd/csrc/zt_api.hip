@@ -1105,6 +1105,20 @@ int zt_synth_u16(zt_ctx* ctx, uint16_t* out, const int64_t* shape, int ndim,
     return ZT_OK;
 }
 
+int zt_reencode_cast(zt_ctx* ctx, int dtype_in, const void* in, int dtype_out, void* out,
+                     int64_t n) {
+    if (int rc = check_ctx(ctx)) return rc;
+    if (zt::dtype_size(dtype_in) == 0 || zt::dtype_size(dtype_out) == 0)
+        return fail(ZT_ERR_UNSUPPORTED_DATA_TYPE, "unsupported data type");
+    if (n < 0) return fail(ZT_ERR_INVALID_PARAMETERS, "negative element count");
+    if (n == 0) return ZT_OK;
+    if (!in || !out) return fail(ZT_ERR_INVALID_PARAMETERS, "null data pointer");
+    DeviceGuard g(ctx->device);
+    hipError_t e = zt::launch_reencode_cast(in, dtype_in, out, dtype_out, n, ctx->cur);
+    if (e != hipSuccess) return hip_fail(e, "reencode cast launch");
+    return ZT_OK;
+}
+
 int zt_synth_box(zt_ctx* ctx, int kind, void* out, const int64_t* start, const int64_t* shape,
                  const int64_t* global_shape, int ndim, uint64_t seed) {
     if (int rc = check_ctx(ctx)) return rc;

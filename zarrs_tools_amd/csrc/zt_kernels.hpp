@@ -54,6 +54,8 @@ std::atomic<int>& fused_variant();
 int fused_tile_y(int radius);  // output tile height of the fused kernel for this radius
 // element-type pairs with a direct fused instantiation; others are staged through f32
 bool fused_direct_pair(int dtype_in, int dtype_out);
+hipError_t launch_reencode_cast(const void* in, int dtype_in, void* out, int dtype_out, int64_t n,
+                                hipStream_t s);
 hipError_t launch_cast_to_f32_3d(const void* in, int dtype, int64_t sz, int64_t sy, float* out,
                                  int64_t nz, int64_t ny, int64_t nx, hipStream_t s);
 hipError_t launch_cast_from_f32_3d(const float* in, int dtype, void* out, int64_t sz, int64_t sy,

@@ -415,6 +415,20 @@ class Downsample:
         output.data.copy_(res.reshape(output.data.shape))
 
 
+def reencode_cast(v, dtype_out: str, ctx: Optional[Context] = None):
+    """Reencode::apply_chunk_convert's element conversion (reencode.rs:58-77) on a device tensor:
+    every element `as` dtype_out (zt_reencode_cast). Returns a new contiguous tensor; bfloat16 is
+    torch.bfloat16."""
+    torch = _torch()
+    v = v.contiguous()
+    ctx = ctx or default_context(v.device.index)
+    dtype_in = dtype_of(v)
+    out = torch.empty(tuple(v.shape), dtype=torch_dtype(dtype_out), device=v.device)
+    check(lib().zt_reencode_cast(ctx.handle, DTYPES[dtype_in], _ptr(v), DTYPES[dtype_out],
+                                 _ptr(out), int(v.numel())))
+    return out
+
+
 def pyramid_level_shapes(shape, factor, max_levels: int) -> list:
     """zarrs_ome.rs:515-560/:731-737 level shapes + stop rule."""
     nd = len(shape)

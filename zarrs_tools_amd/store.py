@@ -190,6 +190,47 @@ def create_output(input_path, output_path, data_type: Optional[str] = None, shap
                                        _enc(encoding)))
 
 
+def host_available_bytes() -> int:
+    """Host memory the store pipeline may budget (as host_available_bytes in host/zt_store.cpp):
+    ZT_STORE_HOST_MEMORY if set, else MemAvailable capped at the cgroup's limit minus its usage."""
+    env = os.environ.get("ZT_STORE_HOST_MEMORY")
+    if env:
+        return int(env)
+    avail = 16 << 30
+    try:
+        with open("/proc/meminfo") as f:
+            for line in f:
+                if line.startswith("MemAvailable:"):
+                    avail = int(line.split()[1]) * 1024
+                    break
+    except OSError:
+        pass
+
+    def _u64(path):
+        try:
+            with open(path) as f:
+                t = f.read().strip()
+            return int(t) if t.isdigit() else None
+        except OSError:
+            return None
+
+    for lim_p, use_p in (("/sys/fs/cgroup/memory.max", "/sys/fs/cgroup/memory.current"),
+                         ("/sys/fs/cgroup/memory/memory.limit_in_bytes",
+                          "/sys/fs/cgroup/memory/memory.usage_in_bytes")):
+        lim, use = _u64(lim_p), _u64(use_p)
+        if lim is not None and use is not None:
+            if lim < (1 << 60):
+                avail = min(avail, max(0, lim - use))
+            break
+    return avail
+
+
+def set_chunk_limit(chunk_limit) -> None:
+    """--chunk-limit for the store filters this thread calls next: at most that many chunks in
+    flight (zt_store_set_chunk_limit; 0 / None = bounded by memory only)."""
+    check(lib().zt_store_set_chunk_limit(int(chunk_limit or 0)))
+
+
 def _flags(erase: bool, finish: bool) -> int:
     return (_abi.STORE_ERASE_OUTPUT_METADATA if erase else 0) | (
         _abi.STORE_FINISH_OUTPUT if finish else 0)
@@ -198,9 +239,11 @@ def _flags(erase: bool, finish: bool) -> int:
 def guided_filter(input_path, output_path, epsilon: float, radius: int,
                   data_type: Optional[str] = None, device: int = 0, rows=None,
                   nthreads: int = 0, erase: bool = True, finish: bool = True,
-                  encoding=None) -> dict:
+                  encoding=None, chunk_limit: int = 0) -> dict:
     """zarrs_filter guided-filter INPUT OUTPUT EPSILON RADIUS [--data-type T] on GPU `device`.
-    `rows` = (begin, end) output chunk rows along axis 0 (None = all). Returns the run stats."""
+    `rows` = (begin, end) output chunk rows along axis 0 (None = all); `chunk_limit` = at most
+    that many chunks in flight (--chunk-limit, 0 = memory-bounded). Returns the run stats."""
+    set_chunk_limit(chunk_limit)
     st = _abi.StoreStats()
     r0, r1 = (0, -1) if rows is None else (int(rows[0]), int(rows[1]))
     check(lib().zt_store_guided_filter(_b(input_path), _b(output_path), _dt(data_type),
@@ -211,8 +254,10 @@ def guided_filter(input_path, output_path, epsilon: float, radius: int,
 
 def downsample(input_path, output_path, stride, discrete: bool = False,
                data_type: Optional[str] = None, device: int = 0, rows=None, nthreads: int = 0,
-               erase: bool = True, finish: bool = True, encoding=None) -> dict:
+               erase: bool = True, finish: bool = True, encoding=None,
+               chunk_limit: int = 0) -> dict:
     """zarrs_filter downsample INPUT OUTPUT STRIDE [--discrete] / one zarrs_ome level."""
+    set_chunk_limit(chunk_limit)
     st = _abi.StoreStats()
     r0, r1 = (0, -1) if rows is None else (int(rows[0]), int(rows[1]))
     check(lib().zt_store_downsample(_b(input_path), _b(output_path), i64_array(stride),
@@ -230,8 +275,9 @@ def _sigma_half(sigma, kernel_half_size):
 
 def gaussian(input_path, output_path, sigma, kernel_half_size, data_type: Optional[str] = None,
              device: int = 0, rows=None, nthreads: int = 0, erase: bool = True,
-             finish: bool = True, encoding=None) -> dict:
+             finish: bool = True, encoding=None, chunk_limit: int = 0) -> dict:
     """zarrs_filter gaussian INPUT OUTPUT SIGMA KERNEL_HALF_SIZE [--data-type T]."""
+    set_chunk_limit(chunk_limit)
     st = _abi.StoreStats()
     r0, r1 = (0, -1) if rows is None else (int(rows[0]), int(rows[1]))
     sg, hs = _sigma_half(sigma, kernel_half_size)
@@ -245,8 +291,9 @@ def gaussian(input_path, output_path, sigma, kernel_half_size, data_type: Option
 def downsample_gaussian(input_path, output_path, stride, sigma, kernel_half_size,
                         data_type: Optional[str] = None, device: int = 0, rows=None,
                         nthreads: int = 0, erase: bool = True, finish: bool = True,
-                        encoding=None) -> dict:
+                        encoding=None, chunk_limit: int = 0) -> dict:
     """One zarrs_ome level with --gaussian-sigma (zarrs_ome.rs:236-271)."""
+    set_chunk_limit(chunk_limit)
     st = _abi.StoreStats()
     r0, r1 = (0, -1) if rows is None else (int(rows[0]), int(rows[1]))
     sg, hs = _sigma_half(sigma, kernel_half_size)

@@ -32,9 +32,11 @@ accelerates:
 
 Filters outside the accelerated path (reencode, crop, rescale, clamp, equal, replace_value,
 gradient_magnitude, summed_area_table) are rejected with FilterError::Other: they are out of scope
-(DESIGN.md §1). `--chunk-limit` bounds the chunks decoded / encoded at once (host worker
-threads); the chunk rows held in memory are bounded by 80 % of the available host and device
-memory, failing like calculate_chunk_limit (filter.rs:52-66) when not even one row fits.
+(DESIGN.md §1). `--chunk-limit N` bounds the chunks in flight (decoded input rows + output rows
+being computed or encoded, and the host worker threads) at N, down to the pipeline's unit of one
+slab and one output row (guided_filter.rs:251-258); independently the rows held in memory are
+bounded by 80 % of the available host and device memory, failing like calculate_chunk_limit
+(filter.rs:52-66) when not even one row fits.
 """
 from __future__ import annotations
 
@@ -279,13 +281,25 @@ def run_device_chain(steps: list, paths: list, device: int = 0, nthreads: int = 
     free, _total = torch.cuda.mem_get_info(device)
     if 2 * peak > budget_frac * free:  # in + out of a step, plus filter scratch of the same order
         return None
+    # the chain input and the last output each pass through one pinned host buffer
+    src0 = S.open_array(paths[0])
+    host_need = max(_nbytes(src0.shape, src0.data_type), _nbytes(plan[-1][2], plan[-1][3]))
+    if host_need > budget_frac * S.host_available_bytes():
+        return None
     results = []
     for k, step in enumerate(steps):
         f, src_info, oshape, odt = plan[k]
         S.create_output(paths[k], paths[k + 1], odt, oshape, encoding_of(step))
+    # The last output is "not finished" (no zarr.json, zarrs_filter.rs:297-313) until its chunks
+    # are written; a failing step leaves no output that looks complete.
+    final_meta = os.path.join(paths[-1], "zarr.json")
+    os.remove(final_meta)
     t0 = time.perf_counter()
     src_info = S.open_array(paths[0])
-    x = read_to_device(paths[0], device, nthreads)
+    try:
+        x = read_to_device(paths[0], device, nthreads)
+    except RuntimeError:  # pinned host or device allocation refused: the store path instead
+        return None
     t_read = time.perf_counter() - t0
     dev = torch.device("cuda", device)
     x_dt, x_chunk = src_info.data_type, src_info.chunk_shape
@@ -308,19 +322,28 @@ def run_device_chain(steps: list, paths: list, device: int = 0, nthreads: int = 
         x, x_dt, x_chunk = y, out_info.data_type, out_info.chunk_shape
     t2 = time.perf_counter()
     write_from_device(paths[-1], x, nthreads)
+    f, _src, oshape, odt = plan[-1]
+    S.create_output(paths[-2], paths[-1], odt, oshape, encoding_of(steps[-1]))  # finished
     results[-1]["encode_s"] = time.perf_counter() - t2
     return results
 
 
-def _rows_worker(name: str, src: str, dst: str, params: dict, device: int, rows, nthreads: int):
+def _rows_worker(name: str, src: str, dst: str, params: dict, device: int, rows, nthreads: int,
+                 env=None):
     """One process of a multi-GPU store step: output chunk rows [rows[0], rows[1]) on `device`,
-    no metadata writes (the parent writes zarr.json once every row is done)."""
+    no metadata writes (the parent writes zarr.json once every row is done). `env`: the memory
+    budget of this process (ZT_STORE_HOST_MEMORY / ZT_STORE_DEVICE_MEMORY, its share)."""
+    os.environ.update(env or {})
     kw = dict(device=device, rows=rows, nthreads=nthreads, erase=False, finish=False,
-              encoding=params.get("encoding"), data_type=params.get("data_type"))
+              encoding=params.get("encoding"), data_type=params.get("data_type"),
+              chunk_limit=params.get("chunk_limit") or 0)
     if name == "guided_filter":
         return S.guided_filter(src, dst, params["epsilon"], params["radius"], **kw)
     if name == "gaussian":
         return S.gaussian(src, dst, params["sigma"], params["kernel_half_size"], **kw)
+    if name == "downsample_gaussian":  # a zarrs_ome level with --gaussian-sigma
+        return S.downsample_gaussian(src, dst, params["stride"], params["sigma"],
+                                     params["kernel_half_size"], **kw)
     return S.downsample(src, dst, params["stride"], discrete=params["discrete"], **kw)
 
 
@@ -341,9 +364,25 @@ def run_rows_parallel(name: str, src: str, dst: str, params: dict, out_shape, gp
     bounds = [(g * nrows // gpus, (g + 1) * nrows // gpus) for g in range(gpus)]
     devices = devices or list(range(gpus))
     per = max(1, (nthreads or min(16, os.cpu_count() or 1)) // gpus)
+    params = dict(params)
+    if params.get("chunk_limit"):  # the reference's limit is per process: split it N ways
+        params["chunk_limit"] = max(1, int(params["chunk_limit"]) // gpus)
+    # each process budgets its share of host memory, and of device memory where processes share
+    # a device (a one-GPU rehearsal), so N processes never reserve N x 80 % together
+    host_share = S.host_available_bytes() // gpus
+    sharing = {d: devices[:gpus].count(d) for d in set(devices[:gpus])}
+    envs = []
+    for g in range(gpus):
+        env = {"ZT_STORE_HOST_MEMORY": str(host_share)}
+        if sharing[devices[g]] > 1 and "ZT_STORE_DEVICE_MEMORY" not in os.environ:
+            import torch
+            free, _ = torch.cuda.mem_get_info(devices[g])
+            env["ZT_STORE_DEVICE_MEMORY"] = str(free // sharing[devices[g]])
+        envs.append(env)
     t0 = time.perf_counter()
     with ProcessPoolExecutor(gpus, mp_context=mp.get_context("spawn")) as ex:
-        futs = [ex.submit(_rows_worker, name, src, dst, params, devices[g], bounds[g], per)
+        futs = [ex.submit(_rows_worker, name, src, dst, params, devices[g], bounds[g], per,
+                          envs[g])
                 for g in range(gpus) if bounds[g][1] > bounds[g][0]]
         parts = [f.result() for f in futs]
     S.create_output(src, dst, params.get("data_type"), out_shape, params.get("encoding"))
@@ -403,7 +442,7 @@ def run(steps: list, exists: str = "erase", tmp: str | None = None,
 
     def store_step(i, step, src, dst):
         name = step.get("filter")
-        threads = step.get("chunk_limit") or chunk_limit or 0
+        limit = step.get("chunk_limit") or chunk_limit or 0  # chunks in flight, not threads
         info = S.open_array(src)
         f, out_shape, _dt = _step_params(step, info)
         enc = encoding_of(step)
@@ -420,22 +459,22 @@ def run(steps: list, exists: str = "erase", tmp: str | None = None,
             params = {"stride": list(f.stride), "discrete": bool(step.get("discrete", False))}
             log(f"{i}: downsample stride={params['stride']} discrete={params['discrete']} "
                 f"{src} ({info.data_type} {list(info.shape)}) -> {dst}")
-        params.update(data_type=step.get("data_type"), encoding=enc)
+        params.update(data_type=step.get("data_type"), encoding=enc, chunk_limit=limit)
         if gpus > 1:
-            st = run_rows_parallel(name, src, dst, params, out_shape, gpus, threads,
+            st = run_rows_parallel(name, src, dst, params, out_shape, gpus, 0,
                                    devices=gpu_devices)
         elif name == "guided_filter":
             st = S.guided_filter(src, dst, params["epsilon"], params["radius"],
                                  data_type=params["data_type"], device=device,
-                                 nthreads=threads, encoding=enc)
+                                 encoding=enc, chunk_limit=limit)
         elif name == "gaussian":
             st = S.gaussian(src, dst, params["sigma"], params["kernel_half_size"],
-                            data_type=params["data_type"], device=device, nthreads=threads,
-                            encoding=enc)
+                            data_type=params["data_type"], device=device, encoding=enc,
+                            chunk_limit=limit)
         else:
             st = S.downsample(src, dst, params["stride"], discrete=params["discrete"],
-                              data_type=params["data_type"], device=device, nthreads=threads,
-                              encoding=enc)
+                              data_type=params["data_type"], device=device, encoding=enc,
+                              chunk_limit=limit)
         out = S.open_array(dst)
         log(f"   -> {out.data_type} {list(out.shape)} in {st['wall_s']:.2f}s "
             f"(rw:{st['decode_s']:.2f}/{st['encode_s']:.2f} p:{st['kernel_s']:.3f})")

@@ -40,6 +40,7 @@ import math
 import os
 import shutil
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -84,6 +85,9 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--group-attributes", default=None)
     ap.add_argument("--exists", choices=["erase", "exit", "overwrite"], default="erase")
     ap.add_argument("--device", type=int, default=0)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="one process per GPU: octant-owned levels (mean / mode), or every "
+                         "level split by output chunk rows (--gaussian-sigma)")
     ap.add_argument("--no-device-resident", action="store_true",
                     help="read every level back from the store (the reference's loop)")
     _add_reencode_args(ap)  # adds --chunk-limit too
@@ -124,39 +128,236 @@ def axis_of(name: str, unit):
     return {"name": name, "unit": unit}
 
 
-def _reencode_level0(src, dst, encoding, nthreads, log):
-    """Reencode::apply for level 0: the input's data in the new encoding, chunk row by chunk row
-    (host copy through the store codecs)."""
-    S.create_output_like(src, dst, encoding.get("data_type"), encoding)
-    out = S.open_array(dst)
+PENDING = ".zt_pending.json"  # metadata of a level not finished yet (host/zt_zarr.hpp)
+
+
+def _hold_metadata(path) -> None:
+    """Hide a new array's zarr.json until its chunks are written (the reference stores the
+    metadata after the chunks, zarrs_ome.rs:729): Zarr readers do not see the array, the store
+    filters of this package still open it."""
+    os.replace(os.path.join(path, "zarr.json"), os.path.join(path, PENDING))
+
+
+def _publish_metadata(path) -> None:
+    os.replace(os.path.join(path, PENDING), os.path.join(path, "zarr.json"))
+
+
+def _reencode_level0(src, dst, encoding, nthreads, log, device: int = 0):
+    """Reencode::apply for level 0 (zarrs_ome.rs:341-366, reencode.rs:128-223): the input's data
+    in the new encoding, chunk row by chunk row; with --data-type every element is converted on
+    the device with the reference's `as` (zt_reencode_cast, reencode.rs:58-77)."""
     info = S.open_array(src)
+    dt_out = encoding.get("data_type") or info.data_type
+    if dt_out not in S.NUMPY:
+        raise _abi.UnsupportedDataType(_abi.ERR_UNSUPPORTED_DATA_TYPE,
+                                       f"unsupported data type {dt_out}")
+    convert = dt_out != info.data_type
+    if convert and not _device_ok(device):
+        raise _abi.FilterError(_abi.ERR_DEVICE, "zarrs_ome --data-type: no HIP device")
+    S.create_output_like(src, dst, dt_out, encoding)
+    _hold_metadata(dst)
+    out = S.open_array(dst)
     cz = out.chunk_shape[0]
+    ctx = None
     for z0 in range(0, info.shape[0], cz):
         n = min(cz, info.shape[0] - z0)
         block = S.read_array(src, [z0] + [0] * (info.ndim - 1), [n] + list(info.shape[1:]),
                              nthreads=nthreads)
-        if out.data_type != info.data_type:
-            raise _abi.InvalidParameters(_abi.ERR_INVALID_PARAMETERS,
-                                         "zarrs_ome level 0: --data-type is not supported")
+        if convert:
+            import torch
+            from . import filter as F
+            ctx = ctx or F.default_context(device)
+            x = torch.from_numpy(block).to(torch.device("cuda", device))
+            if info.data_type == "bfloat16":
+                x = x.view(torch.bfloat16)
+            y = F.reencode_cast(x, dt_out, ctx)
+            if dt_out == "bfloat16":
+                y = y.view(torch.uint16)
+            block = y.cpu().numpy()
         S.write_array(dst, block, [z0] + [0] * (info.ndim - 1), nthreads=nthreads)
+    _publish_metadata(dst)
     log(f"0: reencode {src} -> {dst} ({out.data_type} {list(out.shape)})")
 
 
-def _device_pyramid_fits(info, gauss, device: int, frac: float = 0.8) -> bool:
+def _device_pyramid_fits(info, gauss, device: int, frac: float = 0.8, sharing: int = 1,
+                         host_share: int = 1) -> bool:
     """Level 0 + the pyramid (< 1/7 of level 0 for 2x factors, bounded by level 0 here) + the
-    f32 Gaussian of the largest level, against `frac` of the free device memory."""
+    f32 Gaussian of the largest level, against `frac` of the free device memory (split between
+    `sharing` processes on one device), and level 0's pinned host copy against `frac` of the
+    available host memory (split `host_share` ways)."""
     import torch
     n = int(np.prod(info.shape))
-    need = 2 * n * S.NUMPY[info.data_type]().itemsize + (4 * n if gauss is not None else 0)
+    esz = S.NUMPY[info.data_type]().itemsize
+    need = 2 * n * esz + (4 * n if gauss is not None else 0)
     free, _ = torch.cuda.mem_get_info(device)
-    return need <= frac * free
+    return (need <= frac * free / max(sharing, 1)
+            and n * esz <= frac * S.host_available_bytes() / max(host_share, 1))
+
+
+def _box_chunks(bstart, bshape, chunk, shape):
+    """Chunk-grid index ranges of the chunks a box touches, and its chunk-aligned inner box
+    [i0, i1) (whole chunks inside the box; a chunk cut by the array end counts as whole)."""
+    lo = [b // c for b, c in zip(bstart, chunk)]
+    hi = [-(-(b + n) // c) for b, n, c in zip(bstart, bshape, chunk)]
+    i0 = [-(-b // c) * c for b, c in zip(bstart, chunk)]
+    i1 = [(b + n) if b + n == s else (b + n) // c * c
+          for b, n, c, s in zip(bstart, bshape, chunk, shape)]
+    return lo, hi, i0, i1
+
+
+def _octant_worker(out_root: str, assign, factor, discrete: bool, device: int, nthreads: int,
+                   scratch: str, env=None, compute=None) -> dict:
+    """One process of `zarrs_ome --gpus N` (SURVEY.md §8(e) octant ownership): read this rank's
+    factor^L-aligned level-0 box into HBM, compute levels 1..L of the box there (the windows never
+    cross an aligned box boundary), write every output chunk lying wholly inside the box, and
+    save the pieces of the chunks that cross box boundaries for the host assembly. `compute`
+    (tests only) replaces the device (read box, downsample level) pair."""
+    import numpy as _np
+    os.environ.update(env or {})
+    t0 = time.perf_counter()
+    st = {"rank": assign.rank, "read_s": 0.0, "kernel_s": 0.0, "write_s": 0.0, "pieces": [],
+          "voxels": 0}
+    if assign.coord is None or assign.local_levels == 0:
+        return st
+    lvl0 = os.path.join(out_root, "0")
+    info0 = S.open_array(lvl0)
+    if compute is None:
+        import torch
+        from . import filter as F
+        store_dt = "uint16" if info0.data_type == "bfloat16" else info0.data_type
+        host = torch.empty(tuple(assign.shape), dtype=F.torch_dtype(store_dt), pin_memory=True)
+        S.read_array(lvl0, assign.start, assign.shape, nthreads=nthreads, out=host.numpy())
+        cur = host.to(torch.device("cuda", device), non_blocking=True)
+        torch.cuda.synchronize(device)
+        del host
+        if info0.data_type == "bfloat16":
+            cur = cur.view(torch.bfloat16)
+        ctx = F.default_context(device)
+        ds = F.Downsample(factor, discrete=discrete)
+
+        def level(x):
+            y = ds._apply(x, None, discrete, ctx)
+            ctx.synchronize()
+            return y
+
+        def to_host(x):
+            if x.dtype == torch.bfloat16:
+                x = x.view(torch.uint16)
+            h = torch.empty(tuple(x.shape), dtype=x.dtype, pin_memory=True)
+            h.copy_(x)
+            return h.numpy()
+    else:
+        cur = S.read_array(lvl0, assign.start, assign.shape, nthreads=nthreads)
+        level, to_host = compute, (lambda x: x)
+    st["read_s"] = time.perf_counter() - t0
+    for k in range(1, assign.local_levels + 1):
+        bstart, bshape = assign.level_boxes[k - 1]
+        t1 = time.perf_counter()
+        cur = level(cur)
+        st["kernel_s"] += time.perf_counter() - t1
+        if tuple(cur.shape) != tuple(bshape):
+            raise _abi.FilterError(_abi.ERR_OTHER, f"level {k} box {tuple(cur.shape)} != "
+                                   f"{tuple(bshape)}")
+        t2 = time.perf_counter()
+        path = os.path.join(out_root, str(k))
+        li = S.open_array(path)
+        arr = to_host(cur)
+        st["voxels"] += int(arr.size)
+        lo, hi, i0, i1 = _box_chunks(bstart, bshape, li.chunk_shape, li.shape)
+        if all(b > a for a, b in zip(i0, i1)):
+            sl = tuple(slice(a - b, c - b) for a, c, b in zip(i0, i1, bstart))
+            S.write_array(path, _np.ascontiguousarray(arr[sl]), i0, nthreads=nthreads)
+        # chunks the box only partly covers: this rank's piece of each, assembled by the host
+        for idx in _np.ndindex(*[h - l for l, h in zip(lo, hi)]):
+            cidx = [l + i for l, i in zip(lo, idx)]
+            c0 = [i * c for i, c in zip(cidx, li.chunk_shape)]
+            c1 = [min(a + c, s) for a, c, s in zip(c0, li.chunk_shape, li.shape)]
+            if all(a >= x and b <= y for a, b, x, y in zip(c0, c1, i0, i1)):
+                continue  # written whole above
+            p0 = [max(a, b) for a, b in zip(c0, bstart)]
+            p1 = [min(a, b + n) for a, b, n in zip(c1, bstart, bshape)]
+            if any(b <= a for a, b in zip(p0, p1)):
+                continue
+            sl = tuple(slice(a - b, c - b) for a, c, b in zip(p0, p1, bstart))
+            f = os.path.join(scratch, f"l{k}_r{assign.rank}_{'_'.join(map(str, cidx))}.npy")
+            _np.save(f, _np.ascontiguousarray(arr[sl]))
+            st["pieces"].append((k, tuple(cidx), tuple(p0), f))
+        st["write_s"] += time.perf_counter() - t2
+    st["wall_s"] = time.perf_counter() - t0
+    return st
+
+
+def prepare_octant_levels(out_root: str, level_shapes, local_levels: int) -> None:
+    """Create the level arrays 1..local_levels (each from the previous level's encoding,
+    zarrs_ome.rs:528-560) with their metadata pending until every chunk is written."""
+    for i in range(1, local_levels + 1):
+        src, dst = os.path.join(out_root, str(i - 1)), os.path.join(out_root, str(i))
+        S.create_output(src, dst, None, level_shapes[i - 1],
+                        level_encoding(S.open_array(src), level_shapes[i - 1]))
+        _hold_metadata(dst)
+
+
+def run_octants(out_root: str, shape0, factor, levels, discrete: bool, gpus: int, devices=None,
+                nthreads: int = 0, log=print, compute=None):
+    """Levels 1..L of the pyramid over `gpus` processes, one per GPU, each owning a factor^L-
+    aligned box of level 0 (shard.octant_assignment; no exchange between processes). The level
+    arrays 1..L must exist with pending metadata; chunks crossing box boundaries are assembled
+    on the host (shard.assemble_chunk) and written by this (parent) process. Returns (L, stats)."""
+    import multiprocessing as mp
+    from concurrent.futures import ProcessPoolExecutor
+    from . import shard
+    assigns = [shard.octant_assignment(g, gpus, shape0, factor, levels) for g in range(gpus)]
+    L = assigns[0].local_levels
+    devices = list(devices or range(gpus))
+    per = max(1, (nthreads or min(16, os.cpu_count() or 1)) // gpus)
+    host_share = S.host_available_bytes() // gpus
+    envs = [{"ZT_STORE_HOST_MEMORY": str(host_share)} for _ in range(gpus)]
+    scratch = tempfile.mkdtemp(prefix=".zt_octants_", dir=out_root)
+    t0 = time.perf_counter()
+    try:
+        with ProcessPoolExecutor(gpus, mp_context=mp.get_context("spawn")) as ex:
+            futs = [ex.submit(_octant_worker, out_root, assigns[g], list(factor), discrete,
+                              devices[g], per, scratch, envs[g], compute)
+                    for g in range(gpus) if assigns[g].coord is not None]
+            parts = [f.result() for f in futs]
+        t1 = time.perf_counter()
+        # host assembly of the chunks that cross box boundaries (SURVEY.md §8(e))
+        by_chunk: dict = {}
+        for p in parts:
+            for k, cidx, p0, f in p["pieces"]:
+                by_chunk.setdefault((k, cidx), []).append((p0, f))
+        n_assembled = 0
+        for (k, cidx), pieces in sorted(by_chunk.items()):
+            path = os.path.join(out_root, str(k))
+            li = S.open_array(path)
+            c0 = [i * c for i, c in zip(cidx, li.chunk_shape)]
+            cshape = [min(c, s - a) for a, c, s in zip(c0, li.chunk_shape, li.shape)]
+            arrs = [(p0, np.load(f)) for p0, f in pieces]
+            if sum(a.size for _, a in arrs) != int(np.prod(cshape)):
+                raise _abi.FilterError(_abi.ERR_OTHER, f"level {k} chunk {cidx}: the ranks' "
+                                       "pieces do not cover it")
+            S.write_array(path, shard.assemble_chunk(c0, cshape, arrs), c0, nthreads=nthreads)
+            n_assembled += 1
+    finally:
+        shutil.rmtree(scratch, ignore_errors=True)
+    st = {"wall_s": time.perf_counter() - t0, "assemble_s": time.perf_counter() - t1,
+          "processes": len(parts), "assembled_chunks": n_assembled, "local_levels": L,
+          "grid": list(assigns[0].grid),
+          "per_rank": [{k: v for k, v in p.items() if k != "pieces"} for p in parts]}
+    log(f"   levels 1-{L} on {len(parts)} processes (rank grid {list(assigns[0].grid)}): "
+        f"{st['wall_s']:.2f}s, {n_assembled} chunks assembled on the host")
+    return L, st
 
 
 def run(input_path, output_path, factor=None, max_levels: int = 10, discrete: bool = False,
         name=None, exists: str = "erase", device: int = 0, nthreads: int = 0,
         gaussian_sigma=None, gaussian_kernel_half_size=None, physical_size=None,
         physical_units=None, group_attributes=None, reencoding=None, log=print,
-        device_resident: bool = True) -> dict:
+        device_resident: bool = True, chunk_limit: int = 0, gpus: int = 1,
+        gpu_devices=None) -> dict:
+    """zarrs_ome (zarrs_ome.rs:156-760). gpus > 1: one process per GPU — without a Gaussian the
+    levels are split by octant ownership (run_octants), with one every level is split by output
+    chunk rows (zarrs_filter.run_rows_parallel); `gpu_devices` maps process g to a device."""
     t0 = time.perf_counter()
     info = S.open_array(input_path)
     nd = info.ndim
@@ -177,6 +378,9 @@ def run(input_path, output_path, factor=None, max_levels: int = 10, discrete: bo
         if v is not None and len(v) != nd:
             raise _abi.InvalidParameters(_abi.ERR_INVALID_PARAMETERS,
                                          f"{what} must have one entry per axis")
+    if reencoding and reencoding.get("data_type") and reencoding["data_type"] not in S.NUMPY:
+        raise _abi.UnsupportedDataType(_abi.ERR_UNSUPPORTED_DATA_TYPE,
+                                       f"unsupported data type {reencoding['data_type']}")
     group_attrs = {}
     if group_attributes:
         group_attrs.update(json.loads(group_attributes) if isinstance(group_attributes, str)
@@ -189,7 +393,7 @@ def run(input_path, output_path, factor=None, max_levels: int = 10, discrete: bo
     os.makedirs(output_path, exist_ok=True)
     lvl0 = os.path.join(output_path, "0")
     if reencoding:
-        _reencode_level0(input_path, lvl0, reencoding, nthreads, log)
+        _reencode_level0(input_path, lvl0, reencoding, nthreads, log, device)
     else:
         if os.path.exists(lvl0):
             shutil.rmtree(lvl0)
@@ -213,25 +417,55 @@ def run(input_path, output_path, factor=None, max_levels: int = 10, discrete: bo
     shape = list(S.open_array(lvl0).shape)
     stats = []
     lvl0_info = S.open_array(lvl0)
-    on_device = (device_resident and _device_ok(device)
+    level_shapes = []
+    cur_shape = list(shape)
+    for _ in range(max_levels):  # downsample.rs:162-168 + the stop rule (:731-737)
+        cur_shape = [max(s // f, 1) for s, f in zip(cur_shape, factor)]
+        level_shapes.append(cur_shape)
+        if all(f == 1 or s == 1 for f, s in zip(factor, cur_shape)):
+            break
+    multi = gpus > 1 and _device_ok(device)
+    octants_done = 0  # levels 1..octants_done computed by run_octants
+    if multi and gauss is None and level_shapes:
+        from . import shard
+        devices = list(gpu_devices or range(gpus))[:gpus]
+        boxes = [shard.octant_assignment(g, gpus, shape, factor, len(level_shapes))
+                 for g in range(gpus)]
+        big = max(boxes, key=lambda b: int(np.prod(b.shape)))
+        sharing = max(devices.count(d) for d in devices)
+        box_info = S.ArrayInfo(lvl0, lvl0_info.data_type, tuple(big.shape), (), ())
+        if big.local_levels > 0 and _device_pyramid_fits(box_info, None, devices[0],
+                                                         sharing=sharing, host_share=gpus):
+            prepare_octant_levels(output_path, level_shapes, big.local_levels)
+            octants_done, st_oct = run_octants(output_path, shape, factor, len(level_shapes),
+                                               discrete, gpus, devices, nthreads, log)
+            st_oct["levels"] = octants_done
+            stats.append(st_oct)
+    on_device = (not multi and device_resident and _device_ok(device)
                  and _device_pyramid_fits(lvl0_info, gauss, device))
     cur = None  # the previous level in HBM (device-resident pyramid)
     if on_device:
         from . import filter as F
         ctx = F.default_context(device)
         t1 = time.perf_counter()
-        cur = read_to_device(lvl0, device, nthreads)
+        try:
+            cur = read_to_device(lvl0, device, nthreads)
+        except RuntimeError:  # pinned host or device allocation refused: the store path
+            on_device = False
         log(f"   level 0 -> device in {time.perf_counter() - t1:.2f}s")
-    for i in range(1, max_levels + 1):
+    for i in range(1, len(level_shapes) + 1):
         src, dst = os.path.join(output_path, str(i - 1)), os.path.join(output_path, str(i))
         src_info = S.open_array(src)
-        out_shape = [max(s // f, 1) for s, f in zip(shape, factor)]  # downsample.rs:162-168
+        out_shape = level_shapes[i - 1]
         enc = level_encoding(src_info, out_shape)
-        if on_device:
+        if i <= octants_done:
+            _publish_metadata(dst)
+        elif on_device:
             # the level from the previous one in HBM: (Gaussian, f32) then the downsample, the
             # same kernels as the store path's per-row calls (chunked == whole array)
             t1 = time.perf_counter()
             S.create_output(src, dst, None, out_shape, enc)
+            _hold_metadata(dst)
             v = cur
             if gauss is not None:
                 v = F.Gaussian(gauss[0], gauss[1]).apply_ndarray(v, dtype_out="float32", ctx=ctx)
@@ -242,26 +476,38 @@ def run(input_path, output_path, factor=None, max_levels: int = 10, discrete: bo
             t_k = time.perf_counter() - t1
             t2 = time.perf_counter()
             write_from_device(dst, nxt, nthreads)
-            st = {"wall_s": time.perf_counter() - t1, "decode_s": 0.0,
-                  "encode_s": time.perf_counter() - t2, "h2d_s": 0.0, "kernel_s": t_k,
-                  "d2h_s": 0.0, "voxels": int(nxt.numel()), "device_resident": True}
+            _publish_metadata(dst)
+            stats.append({"wall_s": time.perf_counter() - t1, "decode_s": 0.0,
+                          "encode_s": time.perf_counter() - t2, "h2d_s": 0.0, "kernel_s": t_k,
+                          "d2h_s": 0.0, "voxels": int(nxt.numel()), "device_resident": True})
             cur = nxt
+        elif multi:
+            from .zarrs_filter import run_rows_parallel
+            if gauss is not None:
+                params = {"stride": factor, "sigma": gauss[0], "kernel_half_size": gauss[1],
+                          "encoding": enc, "chunk_limit": chunk_limit}
+                nm = "downsample_gaussian"
+            else:
+                params = {"stride": factor, "discrete": discrete, "encoding": enc,
+                          "chunk_limit": chunk_limit}
+                nm = "downsample"
+            stats.append(run_rows_parallel(nm, src, dst, params, out_shape, gpus,
+                                           devices=gpu_devices))
         elif gauss is not None:
-            st = S.downsample_gaussian(src, dst, factor, gauss[0], gauss[1], device=device,
-                                       nthreads=nthreads, encoding=enc)
+            stats.append(S.downsample_gaussian(src, dst, factor, gauss[0], gauss[1],
+                                               device=device, encoding=enc,
+                                               chunk_limit=chunk_limit))
         else:
-            st = S.downsample(src, dst, factor, discrete=discrete, device=device,
-                              nthreads=nthreads, encoding=enc)
-        stats.append(st)
+            stats.append(S.downsample(src, dst, factor, discrete=discrete, device=device,
+                                      encoding=enc, chunk_limit=chunk_limit))
         out = S.open_array(dst)
         scale = level_scale(scale, shape, out.shape)
         datasets.append({"path": str(i), "coordinateTransformations": [
             {"type": "scale", "scale": list(scale)},
             {"type": "translation", "translation": level_translation(scale)}]})
-        log(f"{i}: {list(shape)} -> {list(out.shape)} in {st['wall_s']:.2f}s")
+        if i > octants_done:
+            log(f"{i}: {list(shape)} -> {list(out.shape)} in {stats[-1]['wall_s']:.2f}s")
         shape = list(out.shape)
-        if all(f == 1 or s == 1 for f, s in zip(factor, shape)):
-            break
     units = physical_units or [None] * nd
     axes = [axis_of(dim_names[k] if dim_names and dim_names[k] is not None else str(k),
                     units[k]) for k in range(nd)]
@@ -281,7 +527,7 @@ def run(input_path, output_path, factor=None, max_levels: int = 10, discrete: bo
     with open(os.path.join(output_path, "zarr.json"), "w") as f:
         json.dump(group, f, indent=2)
     log(f"Output {output_path} in {time.perf_counter() - t0:.2f}s")
-    return {"levels": len(stats), "stats": stats}
+    return {"levels": len(level_shapes), "stats": stats}
 
 
 def main(argv=None) -> int:
@@ -289,9 +535,10 @@ def main(argv=None) -> int:
     enc = encoding_of({k: getattr(a, k, None) for k in REENCODE_KEYS})
     try:
         run(a.input, a.output, a.factor, a.max_levels, a.discrete, a.name, a.exists, a.device,
-            a.filter_chunk_limit or 0, a.gaussian_sigma, a.gaussian_kernel_half_size,
+            0, a.gaussian_sigma, a.gaussian_kernel_half_size,
             a.physical_size, a.physical_units, a.group_attributes, enc,
-            device_resident=not a.no_device_resident)
+            device_resident=not a.no_device_resident, chunk_limit=a.filter_chunk_limit or 0,
+            gpus=a.gpus)
     except _abi.FilterError as e:
         print(f"Error: {e}", file=sys.stderr)
         return 1
