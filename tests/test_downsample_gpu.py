@@ -95,3 +95,33 @@ def test_pyramid_levels_bit_exact():
     for lvl in levels:
         cur = O.downsample(cur, "uint16", (2, 2, 2), "uint16")
         assert np.array_equal(from_dev(lvl, "uint16"), cur)
+
+
+@pytest.mark.parametrize("shape,dtype", [
+    ((37, 50, 71), "uint16"), ((64, 64, 64), "uint8"), ((9, 17, 33), "int16"),
+    ((40, 36, 72), "float32"), ((24, 20, 16), "float64"), ((19, 32, 40), "int64"),
+    ((16, 16, 264), "uint32"), ((70, 8, 8), "int8"), ((5, 300, 9), "uint16")])
+def test_fused_pyramid_levels_equal_per_level_launches(shape, dtype, monkeypatch):
+    """zt_pyramid_downsample fuses up to three 2x2x2 mean levels per launch; every level must be
+    bit-identical to the oracle's level-by-level downsample (odd extents, partial workgroups,
+    unaligned rows, 8- to 64-bit types) and to the unfused launches."""
+    import torch
+    rng = np.random.default_rng(sum(shape))
+    if dtype.startswith("float"):
+        v = (rng.standard_normal(shape) * 1000.0).astype(dtype)
+    else:
+        info = np.iinfo(dtype)
+        v = rng.integers(info.min, info.max, shape, dtype=dtype, endpoint=True)
+    x = to_dev(v, dtype)
+    levels = zt.pyramid(x, (2, 2, 2), max_levels=6)
+    monkeypatch.setenv("ZT_PYRAMID_UNFUSED", "1")
+    plain = zt.pyramid(x, (2, 2, 2), max_levels=6)
+    torch.cuda.synchronize()
+    assert len(levels) == len(plain) == len(zt.pyramid_level_shapes(shape, (2, 2, 2), 6))
+    cur = v
+    for got, ref in zip(levels, plain):
+        cur = O.downsample(cur, dtype, (2, 2, 2), dtype)
+        g = from_dev(got, dtype)
+        assert g.shape == cur.shape
+        np.testing.assert_array_equal(g, cur)
+        np.testing.assert_array_equal(g, from_dev(ref, dtype))

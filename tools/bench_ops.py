@@ -5,8 +5,8 @@ pyramid (config P per GPU: a 2048^3 uint16 octant, factor 2, 5 levels) and the G
 per operation with its HBM roofline fraction and a CPU baseline (the oracle's C restatement,
 one thread, on a bounded sample of the same workload).
 
-Algorithmic bytes: pyramid = every level's input read once + output written once (2 B per u16
-element); Gaussian = 4 B read + 4 B written per voxel (the separable passes' intermediates are
+Algorithmic bytes: pyramid = level 0 read once + every level written once (2 B per u16
+element; the fused launches never read an intermediate level back); Gaussian = 4 B read + 4 B written per voxel (the separable passes' intermediates are
 not credited).
 """
 import argparse
@@ -44,9 +44,12 @@ def bench_pyramid(n, reps, levels):
     shapes = zt.pyramid_level_shapes((n, n, n), (2, 2, 2), levels)
     ms = timed(lambda: zt.pyramid(x, (2, 2, 2), levels, ctx=ctx),
                torch.cuda.current_stream(), reps)
-    prev, nbytes = (n, n, n), 0
+    # compulsory bytes: level 0 read once + every level written once (fused launches never
+    # read an intermediate level back); per_level: each level's input read + output written
+    prev, nbytes, per_level = (n, n, n), 2 * n ** 3, 0
     for s in shapes:
-        nbytes += 2 * (int(np.prod(prev)) + int(np.prod(s)))
+        per_level += 2 * (int(np.prod(prev)) + int(np.prod(s)))
+        nbytes += 2 * int(np.prod(s))
         prev = s
     gbs = nbytes / (ms / 1e3) / 1e9
     # CPU: the oracle's level-1 downsample of a 256^3 sample (single thread)
@@ -59,7 +62,7 @@ def bench_pyramid(n, reps, levels):
             "ms": round(ms, 4), "input_gvox_per_s": round(n ** 3 / (ms / 1e3) / 1e9, 3),
             "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
-                         "algorithmic_bytes": nbytes},
+                         "algorithmic_bytes": nbytes, "per_level_bytes": per_level},
             "cpu_baseline": {"input_gvox_per_s": round(256 ** 3 / cpu_s / 1e9, 4), "cores": 1,
                              "kind": "port", "sample": "level 1 of a 256^3 uint16 block, "
                              "oracle downsample (C restatement of downsample.rs:72-97)"}}

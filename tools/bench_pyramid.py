@@ -11,7 +11,7 @@ a store (not part of this device-resident measurement).
 --gpus N outside a launcher starts the N ranks itself (torch.distributed.run, 127.0.0.1). With
 --size 4096 at N = 1 the single GPU holds the whole 32 GiB volume. Prints one JSON line: input
 Gvox/s over all ranks, the max-over-ranks time per pyramid, the per-GPU algorithmic HBM rate
-(every level's input read once + output written once) and its roofline fraction, and a bit-exact
+(level 0 read once + every level written once) and its roofline fraction, and a bit-exact
 check of one 64^3 block of each level against the oracle (rank 0, outside the timed region)."""
 import argparse
 import json
@@ -88,9 +88,14 @@ def main():
         t = torch.tensor([wall, kern], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall, kern = float(t[0]), float(t[1])
-    prev, nbytes = asg.shape, 0
+    # compulsory bytes (the roofline basis): level 0 read once + every level written once (the
+    # fused launches never read an intermediate level back); per_level_bytes: each level's
+    # input read + output written, as one launch per level moves them
+    prev, per_level = asg.shape, 0
+    nbytes = 2 * int(np.prod(asg.shape))
     for lv in levels:
-        nbytes += 2 * (int(np.prod(prev)) + int(np.prod(lv.shape)))
+        per_level += 2 * (int(np.prod(prev)) + int(np.prod(lv.shape)))
+        nbytes += 2 * int(np.prod(lv.shape))
         prev = tuple(lv.shape)
     res = None
     if rank == 0:
@@ -116,7 +121,8 @@ def main():
                                   "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                   "frac": round(gbs / HBM_PEAK_GBS, 4),
                                   "kernel_ms": round(kern * 1e3, 4),
-                                  "algorithmic_bytes": nbytes},
+                                  "algorithmic_bytes": nbytes,
+                                  "per_level_bytes": per_level},
                "parity": {"bit_exact_sample": ok, "oracle": "oracle downsample of 64^3 blocks"}}
         print(json.dumps(res), flush=True)
     if world > 1:

@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <stdint.h>
+#include <type_traits>
 
 #include "zt_device.hpp"
 #include "zt_kernels.hpp"
@@ -111,6 +112,194 @@ __global__ __launch_bounds__(256) void downsample_discrete_kernel(const TIn* __r
         // integer->float rounds to nearest.
         if constexpr (std::is_integral<TOut>::value) out[o] = (TOut)best;
         else out[o] = from_f64<TOut>((double)best);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Fused 2x2x2 mean pyramid: NL = 2 or 3 levels of zarrs_ome's loop (zarrs_ome.rs:515-738, each
+// level downsample.rs:72-97 of the previous one) in one launch, so the intermediate levels are
+// written once and never read back. Every output is computed exactly as downsample3_kernel does
+// it (C-order f64 sum from -0.0 of the previous level's `as`-rounded values, / 8, `as T`; 8- to
+// 32-bit integers summed exactly in integers, the same value), so the levels are bit-identical
+// to per-level launches.
+//
+// Workgroup = 4 waves; wave w holds (dz, dy) = (w >> 1, w & 1) of a 2x2 block of level-2 rows,
+// lane l the level-3 column x3 = 64 bx + l. A lane reads a 4 x 4 x 8 block of level 0 (sixteen
+// 8-element rows: 16-byte loads for u16, one contiguous KiB per wave-instruction), computes the
+// 2 x 2 x 4 level-1 block, its 2 level-2 values, and (NL = 3) the four waves' level-2 pairs meet
+// in LDS for the level-3 value. The grid covers level 1 (ceil(S1 / (4, 4, 256)) workgroups) so
+// edge elements of level 1 / 2 outside any level-3 window are produced too; an output is stored
+// iff it lies inside its level's shape (its inputs then lie inside theirs).
+// ---------------------------------------------------------------------------------------------
+struct PyrParams {
+    int64_t s[4][3];  // level shapes (z, y, x), level 0 = input
+};
+
+template <typename T>
+constexpr bool kPyrIntSum = std::is_integral<T>::value && sizeof(T) <= 4;
+
+template <typename T>
+__device__ __forceinline__ T pyr_mean8(const T (&v)[8]) {  // v in C order of the window
+    if constexpr (kPyrIntSum<T>) {
+        int64_t s = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) s += (int64_t)v[i];
+        return from_f64<T>((double)s / 8.0);  // = the f64 sum (exact) / 8
+    } else {
+        double s = -0.0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) s += Elem<T>::to_f64(v[i]);
+        return from_f64<T>(s / 8.0);
+    }
+}
+
+template <typename T, int NL, bool VEC>
+__global__ __launch_bounds__(256) void pyramid3_fused_kernel(const T* __restrict__ in,
+                                                             T* __restrict__ l1,
+                                                             T* __restrict__ l2,
+                                                             T* __restrict__ l3, PyrParams p) {
+    __shared__ T lds2[4][64][2];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int dz = w >> 1, dy = w & 1;
+    const int64_t x3 = (int64_t)blockIdx.x * 64 + lane;
+    const int64_t by = blockIdx.y;
+    const int64_t n0y = p.s[0][1], n0x = p.s[0][2];
+    const int64_t n1z = p.s[1][0], n1y = p.s[1][1], n1x = p.s[1][2];
+    const int64_t n2z = p.s[2][0], n2y = p.s[2][1], n2x = p.s[2][2];
+    const int64_t nz1blocks = (n1z + 3) / 4;
+    for (int64_t bz = blockIdx.z; bz < nz1blocks; bz += gridDim.z) {
+        // level-0 block rows: z0 = 8 bz + 4 dz + a, y0 = 8 by + 4 dy + b, x0 = 8 x3 + c; all 16
+        // rows are loaded before any is used (16 loads in flight per lane), kept packed
+        typedef T V8 __attribute__((ext_vector_type(8)));
+        V8 v[4][4];
+        const int64_t z0b = 8 * bz + 4 * dz, y0b = 8 * by + 4 * dy, x0b = 8 * x3;
+        const bool xfull = x0b + 8 <= n0x;
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const int64_t z0 = z0b + a, y0 = y0b + b;
+                const bool rok = z0 < p.s[0][0] && y0 < n0y;  // wave-uniform
+                const T* row = in + (z0 * n0y + y0) * n0x + x0b;
+                if (VEC && rok && xfull) {
+                    v[a][b] = *reinterpret_cast<const V8*>(row);
+                } else {
+#pragma unroll
+                    for (int c = 0; c < 8; ++c) v[a][b][c] = (rok && x0b + c < n0x) ? row[c] : T(0);
+                }
+            }
+        // level 1: the 2 x 2 x 4 block z1 = 4 bz + 2 dz + i, y1 = 4 by + 2 dy + j, x1 = 4 x3 + k
+        T u1[2][2][4];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const T t[8] = {v[2 * i][2 * j][2 * k],     v[2 * i][2 * j][2 * k + 1],
+                                    v[2 * i][2 * j + 1][2 * k], v[2 * i][2 * j + 1][2 * k + 1],
+                                    v[2 * i + 1][2 * j][2 * k], v[2 * i + 1][2 * j][2 * k + 1],
+                                    v[2 * i + 1][2 * j + 1][2 * k],
+                                    v[2 * i + 1][2 * j + 1][2 * k + 1]};
+                    u1[i][j][k] = pyr_mean8<T>(t);
+                }
+        const int64_t z1b = 4 * bz + 2 * dz, y1b = 4 * by + 2 * dy, x1b = 4 * x3;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int64_t z1 = z1b + i, y1 = y1b + j;
+                if (z1 >= n1z || y1 >= n1y) continue;  // wave-uniform
+                T* o = l1 + (z1 * n1y + y1) * n1x + x1b;
+                if constexpr (VEC) {
+                    typedef T V4 __attribute__((ext_vector_type(4)));
+                    if (x1b + 4 <= n1x) {
+                        const V4 q = {u1[i][j][0], u1[i][j][1], u1[i][j][2], u1[i][j][3]};
+                        *reinterpret_cast<V4*>(o) = q;
+                        continue;
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (x1b + k < n1x) o[k] = u1[i][j][k];
+            }
+        // level 2: z2 = 2 bz + dz, y2 = 2 by + dy, x2 = 2 x3 + m
+        T u2[2];
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+            const T t[8] = {u1[0][0][2 * m], u1[0][0][2 * m + 1], u1[0][1][2 * m],
+                            u1[0][1][2 * m + 1], u1[1][0][2 * m], u1[1][0][2 * m + 1],
+                            u1[1][1][2 * m], u1[1][1][2 * m + 1]};
+            u2[m] = pyr_mean8<T>(t);
+        }
+        const int64_t z2 = 2 * bz + dz, y2 = 2 * by + dy, x2 = 2 * x3;
+        if (z2 < n2z && y2 < n2y) {
+            T* o = l2 + (z2 * n2y + y2) * n2x + x2;
+            if (x2 < n2x) o[0] = u2[0];
+            if (x2 + 1 < n2x) o[1] = u2[1];
+        }
+        if constexpr (NL == 3) {
+            lds2[w][lane][0] = u2[0];
+            lds2[w][lane][1] = u2[1];
+            __syncthreads();
+            if (w == 0) {
+                const T t[8] = {lds2[0][lane][0], lds2[0][lane][1], lds2[1][lane][0],
+                                lds2[1][lane][1], lds2[2][lane][0], lds2[2][lane][1],
+                                lds2[3][lane][0], lds2[3][lane][1]};
+                const T u3 = pyr_mean8<T>(t);
+                if (bz < p.s[3][0] && by < p.s[3][1] && x3 < p.s[3][2])
+                    l3[(bz * p.s[3][1] + by) * p.s[3][2] + x3] = u3;
+            }
+            __syncthreads();
+        }
+    }
+}
+
+template <typename T>
+static hipError_t launch_pyr_fused_t(const void* in, void* const* outs, const PyrParams& p,
+                                     int nl, hipStream_t s) {
+    const int64_t gx = (p.s[1][2] + 255) / 256, gy = (p.s[1][1] + 3) / 4;
+    const int64_t gz = std::min<int64_t>((p.s[1][0] + 3) / 4, 65535);
+    if (gx > 0x7FFFFFFF || gy > 65535) return hipErrorInvalidValue;
+    const bool vec = p.s[0][2] % 8 == 0 && (uintptr_t)in % (8 * sizeof(T)) == 0 &&
+                     (uintptr_t)outs[0] % (4 * sizeof(T)) == 0;
+    const dim3 grid((unsigned)gx, (unsigned)gy, (unsigned)gz);
+    const T* i = static_cast<const T*>(in);
+    T* o1 = static_cast<T*>(outs[0]);
+    T* o2 = static_cast<T*>(outs[1]);
+    T* o3 = nl == 3 ? static_cast<T*>(outs[2]) : nullptr;
+    if (nl == 3) {
+        if (vec) hipLaunchKernelGGL((pyramid3_fused_kernel<T, 3, true>), grid, dim3(256), 0, s, i, o1, o2, o3, p);
+        else hipLaunchKernelGGL((pyramid3_fused_kernel<T, 3, false>), grid, dim3(256), 0, s, i, o1, o2, o3, p);
+    } else {
+        if (vec) hipLaunchKernelGGL((pyramid3_fused_kernel<T, 2, true>), grid, dim3(256), 0, s, i, o1, o2, o3, p);
+        else hipLaunchKernelGGL((pyramid3_fused_kernel<T, 2, false>), grid, dim3(256), 0, s, i, o1, o2, o3, p);
+    }
+    return hipGetLastError();
+}
+
+bool pyramid_fused_dtype(int dtype) {
+    return dtype != kBF16 && dtype != kF16 && dtype_size(dtype) > 0;
+}
+
+hipError_t launch_pyramid_fused(const void* in, int dtype, const int64_t (*shapes)[3], int nl,
+                                void* const* outs, hipStream_t s) {
+    if (nl != 2 && nl != 3) return hipErrorInvalidValue;
+    PyrParams p{};
+    for (int l = 0; l <= nl; ++l)
+        for (int d = 0; d < 3; ++d) p.s[l][d] = shapes[l][d];
+    switch (dtype) {
+    case kBool: case kU8: return launch_pyr_fused_t<uint8_t>(in, outs, p, nl, s);
+    case kI8: return launch_pyr_fused_t<int8_t>(in, outs, p, nl, s);
+    case kI16: return launch_pyr_fused_t<int16_t>(in, outs, p, nl, s);
+    case kU16: return launch_pyr_fused_t<uint16_t>(in, outs, p, nl, s);
+    case kI32: return launch_pyr_fused_t<int32_t>(in, outs, p, nl, s);
+    case kU32: return launch_pyr_fused_t<uint32_t>(in, outs, p, nl, s);
+    case kI64: return launch_pyr_fused_t<int64_t>(in, outs, p, nl, s);
+    case kU64: return launch_pyr_fused_t<uint64_t>(in, outs, p, nl, s);
+    case kF32: return launch_pyr_fused_t<float>(in, outs, p, nl, s);
+    case kF64: return launch_pyr_fused_t<double>(in, outs, p, nl, s);
+    default: return hipErrorInvalidValue;
     }
 }
 

@@ -12,6 +12,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -1062,13 +1063,47 @@ int zt_pyramid_downsample(zt_ctx* ctx, int dtype, const void* level0, const int6
     const void* src = level0;
     int64_t cur[ZT_MAX_DIMS];
     std::copy(shape, shape + ndim, cur);
-    for (int i = 0; i < n; ++i) {
+    // 2x2x2 mean levels fuse, up to three per launch, while every extent of a fused level's
+    // input is >= 2 (window 2 on every axis); other levels run one launch each
+    const bool fusable = ndim == 3 && !discrete && factor[0] == 2 && factor[1] == 2 &&
+                         factor[2] == 2 && zt::pyramid_fused_dtype(dtype) &&
+                         std::getenv("ZT_PYRAMID_UNFUSED") == nullptr;
+    auto level_shape = [&](int i) -> const int64_t* {  // shape of level i (0 = input)
+        return i == 0 ? shape : shapes.data() + (size_t)(i - 1) * ndim;
+    };
+    for (int i = 0; i < n;) {
+        int k = 0;
+        while (fusable && k < 3 && i + k < n) {
+            const int64_t* sh = level_shape(i + k);
+            if (sh[0] < 2 || sh[1] < 2 || sh[2] < 2) break;
+            ++k;
+        }
+        if (k >= 2) {
+            int64_t sh3[4][3] = {};
+            for (int l = 0; l <= k; ++l) std::copy(level_shape(i + l), level_shape(i + l) + 3, sh3[l]);
+            bool any = true;
+            for (int d = 0; d < 3; ++d) any = any && sh3[1][d] > 0;
+            if (any) {
+                if (!src || !level_ptrs[i] || !level_ptrs[i + 1] || (k == 3 && !level_ptrs[i + 2]))
+                    return fail(ZT_ERR_INVALID_PARAMETERS, "null level pointer");
+                DeviceGuard g(ctx->device);
+                if (ctx->timed) ZT_HIP(hipEventRecord(ctx->ev0, ctx->cur));
+                hipError_t e = zt::launch_pyramid_fused(src, dtype, sh3, k, level_ptrs + i, ctx->cur);
+                if (e != hipSuccess) return hip_fail(e, "fused pyramid launch");
+                if (ctx->timed) ZT_HIP(hipEventRecord(ctx->ev1, ctx->cur));
+            }
+            src = level_ptrs[i + k - 1];
+            std::copy(level_shape(i + k), level_shape(i + k) + ndim, cur);
+            i += k;
+            continue;
+        }
         // level i+1 = downsample(level i), same dtype in/out (zarrs_ome.rs:211-234)
         int rc = zt_downsample_apply_ndarray(ctx, dtype, src, cur, ndim, factor, discrete, dtype,
                                              level_ptrs[i]);
         if (rc) return rc;
         src = level_ptrs[i];
         std::copy(shapes.data() + (size_t)i * ndim, shapes.data() + (size_t)(i + 1) * ndim, cur);
+        ++i;
     }
     *levels_written = n;
     return ZT_OK;

@@ -225,6 +225,21 @@ def host_available_bytes() -> int:
     return avail
 
 
+PENDING_METADATA = ".zt_pending.json"  # kPendingMetadata, host/zt_zarr.hpp
+
+
+def hold_metadata(path) -> None:
+    """Hide a new array's zarr.json until its chunks are written ("not finished",
+    zarrs_filter.rs:297-313; the reference stores metadata after the chunks): Zarr readers do not
+    see the array, the store functions of this package still open it."""
+    os.replace(os.path.join(path, "zarr.json"), os.path.join(path, PENDING_METADATA))
+
+
+def publish_metadata(path) -> None:
+    """The array is finished: its held metadata becomes zarr.json (an atomic rename)."""
+    os.replace(os.path.join(path, PENDING_METADATA), os.path.join(path, "zarr.json"))
+
+
 def set_chunk_limit(chunk_limit) -> None:
     """--chunk-limit for the store filters this thread calls next: at most that many chunks in
     flight (zt_store_set_chunk_limit; 0 / None = bounded by memory only)."""

@@ -292,8 +292,7 @@ def run_device_chain(steps: list, paths: list, device: int = 0, nthreads: int = 
         S.create_output(paths[k], paths[k + 1], odt, oshape, encoding_of(step))
     # The last output is "not finished" (no zarr.json, zarrs_filter.rs:297-313) until its chunks
     # are written; a failing step leaves no output that looks complete.
-    final_meta = os.path.join(paths[-1], "zarr.json")
-    os.remove(final_meta)
+    S.hold_metadata(paths[-1])
     t0 = time.perf_counter()
     src_info = S.open_array(paths[0])
     try:
@@ -322,8 +321,7 @@ def run_device_chain(steps: list, paths: list, device: int = 0, nthreads: int = 
         x, x_dt, x_chunk = y, out_info.data_type, out_info.chunk_shape
     t2 = time.perf_counter()
     write_from_device(paths[-1], x, nthreads)
-    f, _src, oshape, odt = plan[-1]
-    S.create_output(paths[-2], paths[-1], odt, oshape, encoding_of(steps[-1]))  # finished
+    S.publish_metadata(paths[-1])  # finished
     results[-1]["encode_s"] = time.perf_counter() - t2
     return results
 

@@ -128,18 +128,9 @@ def axis_of(name: str, unit):
     return {"name": name, "unit": unit}
 
 
-PENDING = ".zt_pending.json"  # metadata of a level not finished yet (host/zt_zarr.hpp)
-
-
-def _hold_metadata(path) -> None:
-    """Hide a new array's zarr.json until its chunks are written (the reference stores the
-    metadata after the chunks, zarrs_ome.rs:729): Zarr readers do not see the array, the store
-    filters of this package still open it."""
-    os.replace(os.path.join(path, "zarr.json"), os.path.join(path, PENDING))
-
-
-def _publish_metadata(path) -> None:
-    os.replace(os.path.join(path, PENDING), os.path.join(path, "zarr.json"))
+PENDING = S.PENDING_METADATA  # metadata of a level not finished yet (host/zt_zarr.hpp)
+_hold_metadata = S.hold_metadata
+_publish_metadata = S.publish_metadata
 
 
 def _reencode_level0(src, dst, encoding, nthreads, log, device: int = 0):
