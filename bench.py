@@ -53,6 +53,9 @@ def parse():
     ap.add_argument("--cpu-chunks", type=int, default=0, help="chunks in the CPU sample")
     ap.add_argument("--parity-chunks", type=int, default=6,
                     help="output chunks checked against the oracle after timing (0: skip)")
+    ap.add_argument("--share", default=None, metavar="G/N",
+                    help="1-GPU proxy of one rank of an N-GPU strong split: run only rank G's "
+                         "chunk rows (+ 2r halo) of the volume on this GPU (no process group)")
     ap.add_argument("--radius", type=int, default=RADIUS,
                     help="guided-filter radius (default 4 = the metric; 2 = config G2 at --size 1024)")
     return ap.parse_args()
@@ -212,7 +215,14 @@ def main():
 
     size = args.size
     gshape = (size * world, size, size) if args.scaling == "weak" else (size, size, size)
-    a = zt.slab_assignment(rank, world, gshape[0], CHUNK, 2 * radius)
+    share = None
+    if args.share:  # (G, N): rank G's slab of an N-way split, timed alone on this GPU
+        share = tuple(int(v) for v in args.share.split("/"))
+        if world != 1 or args.scaling != "strong" or not 0 <= share[0] < share[1]:
+            raise SystemExit("--share G/N: one process, strong scaling, 0 <= G < N")
+        a = zt.slab_assignment(share[0], share[1], gshape[0], CHUNK, 2 * radius)
+    else:
+        a = zt.slab_assignment(rank, world, gshape[0], CHUNK, 2 * radius)
     stream = torch.cuda.current_stream(dev)
     ctx = zt.Context(local, stream)
 
@@ -257,14 +267,14 @@ def main():
         wall, kern_ms = float(tt[0]), float(tt[1])
 
     voxels_rank = a.out_nz * size * size  # rank 0's share (the largest, or equal)
-    voxels_all = gshape[0] * size * size
+    voxels_all = gshape[0] * size * size if share is None else voxels_rank
     ms_per_step = wall * 1000.0 / args.steps
     value = voxels_all * 4 / 2 ** 30 / (ms_per_step / 1000.0)
     achieved = voxels_rank * ALGO_BYTES_PER_VOXEL / (kern_ms / 1000.0) / 1e9  # GB/s per GPU
     traffic = load_traffic(gshape, radius, world)
 
-    headline = (size == N and radius == 4 and args.scaling == "strong") or (
-        world == 1 and size == N and radius == 4)
+    headline = share is None and ((size == N and radius == 4 and args.scaling == "strong") or (
+        world == 1 and size == N and radius == 4))
     res = {
         "metric": BASELINE_METRIC if headline else
         f"GiB/s filtered (device-resident), guided_filter r={radius}, {size}³ f32, "
@@ -294,7 +304,14 @@ def main():
                      "kernel_ms": round(kern_ms, 4),
                      "algorithmic_bytes_per_launch": voxels_rank * ALGO_BYTES_PER_VOXEL},
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if share is not None:
+        res["metric"] += f", rank {share[0]}'s share of a {share[1]}-GPU split (1-GPU proxy)"
+        res["config"]["parallelism"] = f"share {share[0]}/{share[1]} on one GPU"
+        res["share"] = {"rank": share[0], "world": share[1], "out_z": [a.out_z0, a.out_z0 + a.out_nz],
+                        "in_z": [a.in_z0, a.in_z0 + a.in_nz],
+                        # what N such GPUs would aggregate if every share ran this fast
+                        "projected_aggregate_gibs": round(value * share[1], 3)}
+    if rank == 0 and world == 1 and share is None and not args.no_cpu_baseline:
         try:
             res["cpu_baseline"] = cpu_baseline(gshape, radius, args.cpu_chunks)
         except Exception as e:  # the baseline is reported, never required

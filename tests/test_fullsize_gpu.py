@@ -9,7 +9,8 @@ compared bit-exactly with the oracle's downsample of the same input region (down
   G2  guided_filter r=2, 1024^3 f32, 256^3 chunks        (BASELINE configs[1])
   G3  guided_filter r=4, 2048^3 f32, 256^3 chunks        (configs[2], the metric)
   P   5-level 2x mean pyramid of a 2048^3 u16 per-GPU octant of configs[3]'s 4096^3
-  T   one GPU's (4, 1024^3) f32 share of configs[4], chunks (4, 256^3), r=2
+  T   one GPU's share of configs[4]: output timepoints [8, 12) of (32, 1024^3) f32 from its
+      (12, 1024^3) input block (the 2r t-halo), chunks (4, 256^3), r=2
   2-D 32768 x 16384 f32 (planes of 2 GiB: routed off the 32-bit fused path)
 """
 import numpy as np
@@ -119,14 +120,22 @@ def test_p_pyramid_2048_u16_levels_bit_exact():
 
 
 def test_t_share_4d_sampled_chunks():
+    """Config T's real per-GPU share (output chunk rows along t): output
+    timepoints [8, 12) of the (32, 1024^3) series. The rank holds its input block, timepoints
+    [4, 16) = the output row plus the 2r t-halo, generated from the global synthetic definition
+    (zt_synth_box); every window clamps at the global array, which inside this block is the
+    block's own bounds (the halo is complete), so the middle chunk row of the block equals the
+    reference's per-chunk result of the global array."""
     import torch
-    shape, chunk, r = (4, 1024, 1024, 1024), (4, 256, 256, 256), 2
-    x = zt.synth_step_noise_f32(shape)
-    y = torch.empty_like(x)
-    zt.GuidedFilter(EPS, r).apply(zt.DeviceArray(x, chunk), zt.DeviceArray(y, chunk))
+    gshape, chunk, r = (32, 1024, 1024, 1024), (4, 256, 256, 256), 2
+    t0, tin = 4, 12
+    x = zt.synth_box((t0, 0, 0, 0), (tin,) + gshape[1:], gshape, kind="float32")
+    y = torch.zeros_like(x)
+    zt.GuidedFilter(EPS, r).apply(zt.DeviceArray(x, chunk), zt.DeviceArray(y, chunk),
+                                  chunk_grid_start=(1, 0, 0, 0), chunk_grid_count=(1, 4, 4, 4))
     torch.cuda.synchronize()
     del x
-    _check_chunks(y, shape, chunk, r, [(0, 0, 0, 0), (0, 1, 2, 3), (0, 3, 3, 3)])
+    _check_chunks(y, gshape, chunk, r, [(2, 0, 0, 0), (2, 1, 2, 3), (2, 3, 3, 3)], z_off=t0)
 
 
 def test_2d_plane_of_2gib_routes_off_the_fused_path():

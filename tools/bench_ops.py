@@ -129,6 +129,46 @@ def bench_guided4d(shape, chunk, radius, reps):
                              "guided filter (C restatement of guided_filter.rs)"}}
 
 
+def bench_t_share(reps, radius=2):
+    """Config T's real per-GPU share (SURVEY.md §8(e), rows along t): output timepoints [8, 12)
+    of the (32, 1024^3) f32 series, computed from the rank's (12, 1024^3) input block (the 2r
+    t-halo) generated from the global synthetic definition; the chunk grid of the block's middle
+    row (64 chunks of (4, 256^3)) through GuidedFilter::apply's per-chunk path. Algorithmic bytes:
+    8 per OUTPUT voxel (the t-halo reads are not credited)."""
+    import numpy as np
+    import torch
+    import zarrs_tools_amd as zt
+    from oracle import oracle as O
+    ctx = zt.default_context(0)
+    gshape, chunk, t0, tin = (32, 1024, 1024, 1024), (4, 256, 256, 256), 4, 12
+    x = zt.synth_box((t0, 0, 0, 0), (tin,) + gshape[1:], gshape, kind="float32", ctx=ctx)
+    y = torch.zeros_like(x)
+    g = zt.GuidedFilter(2500.0, radius)
+    a_in, a_out = zt.DeviceArray(x, chunk), zt.DeviceArray(y, chunk)
+    ms = timed(lambda: g.apply(a_in, a_out, ctx=ctx, chunk_grid_start=(1, 0, 0, 0),
+                               chunk_grid_count=(1, 4, 4, 4)),
+               torch.cuda.current_stream(), reps)
+    n = 4 * 1024 ** 3
+    gbs = n * 8 / (ms / 1e3) / 1e9
+    # parity: one interior chunk of the share against the oracle's per-chunk result
+    (o0, osh, ref), = O.guided_filter_synth_chunks(gshape, chunk, [(2, 1, 2, 3)], 2500.0, radius,
+                                                   nthreads=16)
+    got = y[o0[0] - t0:o0[0] - t0 + 4, o0[1]:o0[1] + 256, o0[2]:o0[2] + 256,
+            o0[3]:o0[3] + 256].cpu().numpy()
+    rel = float((np.abs(got.astype(np.float64) - ref) / np.maximum(1.0, np.abs(ref))).max())
+    del x, y
+    torch.cuda.empty_cache()
+    return {"op": f"guided_filter r={radius} 4-D, config T per-GPU share (device-resident)",
+            "config": {"global_shape": list(gshape), "input_block_t": [t0, t0 + tin],
+                       "output_t": [t0 + 4, t0 + 8], "dtype": "float32", "chunk": list(chunk),
+                       "eps": 2500.0, "path": "per chunk (12, 264^3) input, four-kernel 4-D"},
+            "ms": round(ms, 4), "gib_per_s": round(n * 4 / 2 ** 30 / (ms / 1e3), 3),
+            "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
+                         "algorithmic_bytes": n * 8},
+            "parity_max_rel": rel}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--pyramid-size", type=int, default=2048)
@@ -136,9 +176,11 @@ def main():
     ap.add_argument("--levels", type=int, default=5)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--t-shape", type=int, nargs=4, default=[4, 1024, 1024, 1024])
-    ap.add_argument("--only", default="pyramid,gaussian,guided4d")
+    ap.add_argument("--only", default="pyramid,gaussian,tshare")
     a = ap.parse_args()
     only = set(a.only.split(","))
+    if "tshare" in only:
+        print(json.dumps(bench_t_share(a.reps)), flush=True)
     if "guided4d" in only:
         print(json.dumps(bench_guided4d(a.t_shape, (4, 256, 256, 256), 2, a.reps)), flush=True)
         if only == {"guided4d"}:

@@ -1,4 +1,4 @@
-// gf_fused.hpp — the fused 2.5-D guided-filter kernel template (see guided_filter.hip for the
+// tools/gf_fused_variants.hpp — the round-2 fused guided-filter kernel WITH its measured-slower variant switches (GF_ONEBAR, GF_OCT, ...) and ablation flags (ABL), kept for the A/B harnesses in tools/ (not a product path; the product kernel is zarrs_tools_amd/csrc/gf_fused.hpp).
 // design notes). Instantiated per radius in gf_fused_r<R>.hip so the instantiations compile in
 // parallel; guided_filter.hip dispatches.
 #pragma once
@@ -11,19 +11,23 @@
 #include <algorithm>
 #include <type_traits>
 
-#include "zt_device.hpp"
-#include "zt_kernels.hpp"
+#include "../zarrs_tools_amd/csrc/zt_device.hpp"
+#include "../zarrs_tools_amd/csrc/zt_kernels.hpp"
 
-// Tuning knobs (tools/timek.hip sweeps them with -D; profiles/r02_ab_harness.txt). Variants that
-// were measured slower live only in tools/gf_fused_variants.hpp.
+#ifndef GF_T3_TOP
+#define GF_T3_TOP 1
+#endif
 #ifndef GF_K4_R4
-#define GF_K4_R4 8  // r = 4: P4 outputs per item (8 x per item, -2 %)
+#define GF_K4_R4 8
 #endif
 #ifndef GF_ORDER_R4
-#define GF_ORDER_R4 2  // r = 4: P4 issued ahead of P12 in C1 (-2 %)
+#define GF_ORDER_R4 2
 #endif
 #ifndef GF_PRIO
 #define GF_PRIO 1  // s_setprio phase reordering (measured -4.5% at 2048^3 r=4 with the b128 Hx writes)
+#endif
+#ifndef GF_ORDER
+#define GF_ORDER 0
 #endif
 #ifndef GF_HX_B128
 #define GF_HX_B128 1  // 16-byte Hx writes for even R (fewer LDS bank conflicts: -2% at r=4)
@@ -34,6 +38,27 @@
 #ifndef GF_K4
 #define GF_K4 4  // P4 outputs per thread (row segment of the (a, b) x-window)
 #endif
+#ifndef GF_DIRECT
+#define GF_DIRECT 1  // P3 / P5 load their v values and P5 stores its outputs directly (no Lc /
+                     // Lv5 / Lout LDS staging)
+#endif
+#ifndef GF_ONEBAR
+#define GF_ONEBAR 0  // (measured slower: 34.4 vs 32.6 ms) one barrier per z-step: every wave runs P12(i+1), P5(i-2), P3(i), P4(i-1)
+                     // on double-buffered Hx / Lab / Hab (when they fit the LDS; needs GF_DIRECT)
+#endif
+#ifndef GF_OCT
+#define GF_OCT 0  // 8 x per P12 lane: fewer instructions, but concentrated on half the waves
+                  // (measured slower: 35.0 vs 31.7 ms)
+#endif
+#ifndef GF_P3_SPREAD
+#define GF_P3_SPREAD 0  // measured slower (34.1 vs 31.8 ms): the extra issue outweighs the balance
+#endif
+#ifndef GF_V5_AUX
+#define GF_V5_AUX 0  // cache policy of P5's v loads (the last read of an input slice)
+#endif
+#ifndef GF_LEAVE_AUX
+#define GF_LEAVE_AUX 0  // cache policy of P1's leaving-slice loads
+#endif
 #ifndef GF_STX
 #define GF_STX 4  // XCD super-tile: tiles along x (4 x 16 measured best: 31.2 vs 31.9 ms for 8 x 4)
 #endif
@@ -42,6 +67,23 @@
 #endif
 #ifndef GF_WAVE_SKIP
 #define GF_WAVE_SKIP 1  // P4: idle waves branch around the phase
+#endif
+#ifndef GF_NEWTON_A
+#define GF_NEWTON_A 0  // a = s / (s + eps): Markstein's correction on v_rcp_f32 (<= 1 ulp) without
+                       // the Newton step on the reciprocal (a enters only f32 window sums)
+#endif
+#ifndef GF_FASTDIV5
+#define GF_FASTDIV5 1  // stage-2 means as sum * RN(1/count) (one multiply; the sums already
+                       // differ from the reference's f64 SAT sums by a few ulp)
+#endif
+#ifndef GF_PW_SYNC
+#define GF_PW_SYNC 0  // pointwise pairs advanced op by op (no s_nop between dependent v_pk_*)
+#endif
+#ifndef GF_TREE
+#define GF_TREE 1  // f64 window sums as a balanced tree + independent differences (short chains)
+#endif
+#ifndef GF_A_RCP
+#define GF_A_RCP 0  // a = s * rcp(s + eps) without Markstein's correction (<= 2 ulp)
 #endif
 
 namespace zt {
@@ -255,23 +297,36 @@ struct RingDispatch<W, W> {
 // ---------------------------------------------------------------------------------------------
 template <int R, int K>
 __device__ __forceinline__ void slide_sums_f64(const double (&in)[K + 2 * R], double (&out)[K]) {
-    // exact sums: any association gives the same value, so the first window is a balanced
-    // tree and each later one adds an independently formed difference (chain depth
-    // log2(W) + K - 1 instead of 2R + 2(K - 1))
-    double c[2 * R + 1];
+    if constexpr (GF_TREE) {
+        // exact sums: any association gives the same value, so the first window is a balanced
+        // tree and each later one adds an independently formed difference (chain depth
+        // log2(W) + K - 1 instead of 2R + 2(K - 1))
+        double c[2 * R + 1];
 #pragma unroll
-    for (int j = 0; j <= 2 * R; ++j) c[j] = in[j];
+        for (int j = 0; j <= 2 * R; ++j) c[j] = in[j];
 #pragma unroll
-    for (int w = 1; w <= 2 * R; w *= 2) {
+        for (int w = 1; w <= 2 * R; w *= 2) {
 #pragma unroll
-        for (int j = 0; j + w <= 2 * R; j += 2 * w) c[j] = c[j] + c[j + w];
+            for (int j = 0; j + w <= 2 * R; j += 2 * w) c[j] = c[j] + c[j + w];
+        }
+        double d[K];
+#pragma unroll
+        for (int i = 1; i < K; ++i) d[i] = in[i + 2 * R] - in[i - 1];
+        out[0] = c[0];
+#pragma unroll
+        for (int i = 1; i < K; ++i) out[i] = out[i - 1] + d[i];
+    } else {
+        double s = in[0];
+#pragma unroll
+        for (int j = 1; j <= 2 * R; ++j) s += in[j];
+        out[0] = s;
+#pragma unroll
+        for (int i = 1; i < K; ++i) {
+            s = s + in[i + 2 * R];
+            s = s - in[i - 1];
+            out[i] = s;
+        }
     }
-    double d[K];
-#pragma unroll
-    for (int i = 1; i < K; ++i) d[i] = in[i + 2 * R] - in[i - 1];
-    out[0] = c[0];
-#pragma unroll
-    for (int i = 1; i < K; ++i) out[i] = out[i - 1] + d[i];
 }
 
 // s / (s + eps): rcp + one Newton step + Markstein correction (6 VALU ops instead of the ~12 of
@@ -291,6 +346,11 @@ __device__ __forceinline__ float fast_div(float x, float d) {
 // kernel keeps in flight across the barrier.
 __device__ __forceinline__ void lds_barrier() {
     __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+template <int ABL>
+__device__ __forceinline__ void lds_barrier_abl() {
+    if constexpr (ABL & 16) __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    else lds_barrier();
 }
 
 // x / d for an integer count d given rcp = RN(1/d): Markstein's correction step makes the
@@ -461,14 +521,16 @@ struct GFConfig {
     // P12 in C1 (each -2 % at 2048^3, tools/timek.sh); other radii keep the defaults (unmeasured)
     static constexpr bool R4 = R == 4 && TY == 32 && NT == 1024;
     static constexpr int K3 = GF_K3, K4 = R4 ? GF_K4_R4 : GF_K4;
-    static constexpr int ORDER = R4 ? GF_ORDER_R4 : 0;
+    static constexpr int ORDER = R4 ? GF_ORDER_R4 : GF_ORDER;
     static constexpr int K5 = TX * TY / NT;          // outputs per thread (ring width)
     static constexpr int S3 = (E1Y + K3 - 1) / K3;   // segments per column, P3
     static constexpr int S4 = TX / K4;               // segments per row, P4
     static constexpr int N3 = E1X * S3, N4 = E1Y * S4;  // work items
     // P12: one lane per quad (4 consecutive x) of an E2 row, whole rows per wave, so the
     // x-neighbour quads of the window sums come from adjacent lanes (DPP), never across waves
-    static constexpr int QPL = 1;  // quads per lane
+    // GF_OCT: 8 consecutive x per lane (two quads) where E2 rows are whole octets: half the
+    // DPP moves and fewer sliding-sum adds per x-sum output
+    static constexpr int QPL = (GF_OCT && E2X % 8 == 0 && R <= 8) ? 2 : 1;  // quads per lane
     static constexpr int EPL = 4 * QPL;                    // elements per lane
     static constexpr int NQ1X = E2X / EPL;                 // lanes per E2 row
     static constexpr int RPW = 64 / NQ1X;                  // E2 rows per wave
@@ -477,65 +539,86 @@ struct GFConfig {
     // single pass: P12 rows on the top waves (P4 works on the bottom ones)
     static constexpr int W12 = NQP1 == 1 ? NWAVE - (E2Y + RPW - 1) / RPW : 0;
     static constexpr int NB = (R + EPL - 1) / EPL;         // neighbour lanes on each side
-    static constexpr int NQ5 = TX / 4 * TY;                  // output tile quads
+    static constexpr int XC = R % 4;  // Lc quad grid starts XC elements left of the E1 apron
+    static constexpr int NQCX = (E1X + XC + 3) / 4, NQC = NQCX * E1Y;  // Lc: the E1 apron
+    static constexpr int PC = 4 * NQCX;                      // Lc pitch (floats)
+    static constexpr int NQ5 = TX / 4 * TY;                  // v5 / output tile quads
     static constexpr int W3 = W * W * W;                     // interior window count
     static constexpr int al(int b) { return (b + 255) / 256 * 256; }
     static constexpr int SZ_HX = al((E2Y + K3) * PH * 8);
     static constexpr int SZ_LAB = al((E1Y + 1) * PA * 8);
     static constexpr int SZ_HAB = al((E1Y + 1) * PB * 8);
+    static constexpr int SZ_LC = GF_DIRECT ? 0 : al(E1Y * PC * 4);
+    static constexpr int SZ_T = GF_DIRECT ? 0 : al(TY * TX * 4);
     static constexpr int SZ_RCP = al((W3 + 1) * 4);  // RN(1/c) for window counts c <= W^3
-    static constexpr int OFF_HX = 0, OFF_LAB = OFF_HX + SZ_HX;
-    static constexpr int OFF_HAB = OFF_LAB + SZ_LAB;
-    static constexpr int OFF_RCP = OFF_HAB + SZ_HAB;
-    static constexpr int LDS_BYTES = OFF_RCP + SZ_RCP;
+    // single-barrier pipeline: Hx / Lab / Hab double-buffered by step parity, if they fit
+    static constexpr bool ONEBAR = GF_ONEBAR && GF_DIRECT &&
+                                   2 * (SZ_HX + SZ_LAB + SZ_HAB) + SZ_RCP + 256 <= 160 * 1024;
+    static constexpr int NBUF = ONEBAR ? 2 : 1;
+    static constexpr int OFF_HX = 0, OFF_LAB = OFF_HX + NBUF * SZ_HX;
+    static constexpr int OFF_HAB = OFF_LAB + NBUF * SZ_LAB;
+    static constexpr int OFF_LC = OFF_HAB + NBUF * SZ_HAB, OFF_LV5 = OFF_LC + SZ_LC;
+    static constexpr int OFF_LOUT = OFF_LV5 + SZ_T, OFF_RCP = OFF_LOUT + SZ_T;
+    static constexpr int OFF_DUMMY = OFF_RCP + SZ_RCP;  // 16-B sink for inactive lanes' writes
+    static constexpr int LDS_BYTES = OFF_DUMMY + 256;
     // item -> thread placement: heavy phases on different waves (see C0 / C1)
-    static constexpr int T3 = NT - N3;  // first thread of the P3 items (the top N3 threads)
+    static constexpr int T3 = GF_T3_TOP ? NT - N3 : 0;  // first thread of the P3 items
+    // (the bottom placement is not maintained: its P3 loads disagree with GF_DIRECT's item map)
+    static_assert(GF_T3_TOP || !GF_DIRECT, "GF_T3_TOP=0 needs GF_DIRECT=0");
     static_assert(TX * TY % NT == 0, "tile must divide evenly over the threads");
     static_assert(TY % K5 == 0, "ring segment must divide the tile height");
     static_assert(TX % K4 == 0, "P4 segment must divide the tile width");
     static_assert(N3 <= NT && N4 <= NT, "one work item per thread per phase");
     static_assert(RPW >= 1, "an E2 row fits one wave");
+    static_assert(GF_DIRECT || (NQC <= NT && NQ5 <= NT), "one staging quad per thread");
     static_assert(E2X % 4 == 0, "E2 rows are whole quads");
     static_assert(E2X % EPL == 0, "E2 rows are whole lane items");
     static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 };
 
-// MODE 0 (interior): the tiles [itx0, itx1) x [ity0, ity1) whose whole apron lies inside the
-//   domain and whose output tile lies inside the output box: unmasked 16-byte accesses, and the
-//   window counts depend on z only, so they are computed once per step (wave-uniform) and P3 / P5
-//   carry no per-lane count or zeroing logic and no branch.
-// MODE 1 (quad): every other tile of a quad-aligned geometry (each 4-element quad of a global
-//   access wholly inside or wholly outside the domain / output box): unmasked accesses, the
-//   outside quads through kBadOff, per-lane clamped counts and zeroing.
-// MODE 2 (edge): every other tile otherwise: element-wise masked accesses.
-// The grid of modes 1 and 2 covers all tiles; the interior ones return at once. Separate kernels
-// rather than runtime branches keep each march free of control flow around its memory
-// instructions, so the compiler's vmcnt accounting stays exact (a branch there made it drain
-// every load).
-template <int R, int TY, int NT, typename TIn, typename TOut, int MODE>
+// EDGE = false: the tiles [itx0, itx1) x [ity0, ity1), where every 4-element quad of a global
+// access is either entirely inside the domain / output box or entirely outside (all tiles when
+// the geometry is quad-aligned, else the interior tiles): unmasked 16-byte accesses, the
+// outside quads through kBadOff. EDGE = true: every other tile (the grid covers all tiles;
+// those of the first launch return at once), element-wise masked accesses. Two kernels rather
+// than a runtime branch keep each march free of control flow around its memory instructions,
+// so the compiler's vmcnt accounting stays exact (a branch there made it drain every load).
+template <int R, int TY, int NT, typename TIn, typename TOut, bool EDGE, int ABL = 0>
 __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     using C = GFConfig<R, TY, NT>;
-    constexpr bool EDGE = MODE == 2, INTERIOR = MODE == 0;
     constexpr int TX = C::TX, W = C::W;
     constexpr int K5 = C::K5;
     constexpr int ESZ = (int)sizeof(TIn), OSZ = (int)sizeof(TOut);
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    double* const Hx = reinterpret_cast<double*>(smem + C::OFF_HX);
-    float2* const Lab = reinterpret_cast<float2*>(smem + C::OFF_LAB);
-    float2* const Hab = reinterpret_cast<float2*>(smem + C::OFF_HAB);
-    float* const rcp_tab = reinterpret_cast<float*>(smem + C::OFF_RCP);
+    // (re-pointed at the buffer of the step's parity before each phase when C::ONEBAR)
+    double* Hx = reinterpret_cast<double*>(smem + C::OFF_HX);
+    float2* Lab = reinterpret_cast<float2*>(smem + C::OFF_LAB);
+    float2* Hab = reinterpret_cast<float2*>(smem + C::OFF_HAB);
+    auto set_hx = [&](int i) {
+        Hx = reinterpret_cast<double*>(smem + C::OFF_HX + (i & 1) * C::SZ_HX);
+    };
+    auto set_lab = [&](int i) {
+        Lab = reinterpret_cast<float2*>(smem + C::OFF_LAB + (i & 1) * C::SZ_LAB);
+    };
+    auto set_hab = [&](int i) {
+        Hab = reinterpret_cast<float2*>(smem + C::OFF_HAB + (i & 1) * C::SZ_HAB);
+    };
+    float* Lc = reinterpret_cast<float*>(smem + C::OFF_LC);
+    float* Lv5 = reinterpret_cast<float*>(smem + C::OFF_LV5);
+    float* Lout = reinterpret_cast<float*>(smem + C::OFF_LOUT);
+    float* rcp_tab = reinterpret_cast<float*>(smem + C::OFF_RCP);
     // Correctly rounded reciprocals of every possible window count, for div_by_count
-    // (Markstein's correction needs RN(1/c) exactly). Published by the prologue's barrier.
+    // (Markstein's correction needs RN(1/c) exactly). Published by the prologue's barriers.
     for (int c = threadIdx.x; c <= C::W3; c += NT) rcp_tab[c] = c > 0 ? 1.0f / (float)c : 0.0f;
 
     // XCD-aware block -> tile. Blocks b and b+8 share an XCD; give each XCD a contiguous run of
-    // logical ids and walk them in GF_STX x GF_STY-tile super-tiles, so the WGs resident on one
-    // XCD cover a compact region whose xy aprons and z reloads stay in that XCD's 4 MB L2.
+    // logical ids and walk them in 8x4-tile super-tiles, so the WGs resident on one XCD cover a
+    // compact 512x128 region whose xy aprons and z reloads stay in that XCD's 4 MB L2.
     const int nwg = gridDim.x;
     const int b = blockIdx.x;
     const int lid = (nwg % 8 == 0) ? (b % 8) * (nwg / 8) + b / 8 : b;
-    const int gtx = INTERIOR ? p.itx1 - p.itx0 : p.tiles_x;  // this launch's tile grid
-    const int gty = INTERIOR ? p.ity1 - p.ity0 : p.tiles_y;
+    const int gtx = EDGE ? p.tiles_x : p.itx1 - p.itx0;  // this launch's tile grid
+    const int gty = EDGE ? p.tiles_y : p.ity1 - p.ity0;
     const int ntiles = gtx * gty;
     const int seg = lid / ntiles;
     int t = lid % ntiles;
@@ -561,11 +644,11 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
             tile_y = full_y + t / gtx;
         }
     }
-    if constexpr (INTERIOR) {
+    if constexpr (EDGE) {
+        if (tile_x >= p.itx0 && tile_x < p.itx1 && tile_y >= p.ity0 && tile_y < p.ity1) return;
+    } else {
         tile_x += p.itx0;
         tile_y += p.ity0;
-    } else {
-        if (tile_x >= p.itx0 && tile_x < p.itx1 && tile_y >= p.ity0 && tile_y < p.ity1) return;
     }
 
     const int x0 = p.ox0 + tile_x * TX;
@@ -591,12 +674,19 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     };
 
     const int zc_begin = zo_begin - R, zc_end = zo_end + R;  // stage-1 slices of this march
+    // Interior tiles (see launch_fused_cfg): window counts are W^3 wherever z is interior too,
+    // so P3/P5 take a branch-free path with the constant correctly rounded 1/W^3
+    // (host-computed).
+    const bool xy_interior = x0 - 2 * R >= 0 && x0 + TX + 2 * R <= nx && y0 - 2 * R >= 0 &&
+                             y0 + TY + 2 * R <= ny;  // wave-uniform
+    constexpr float kW3 = (float)C::W3;
+    const float rcp_w3 = p.rcp_w3;
 
     // ---- per-thread, step-invariant quad offsets and in-domain masks -----------------------
     const int tid0 = threadIdx.x;
-    constexpr int EPL = C::EPL;
-    int q1off[C::NQP1], q1mask[C::NQP1];
-    // P12 lane -> (E2 row, lane item = 4 consecutive x) for pass k
+    constexpr int QPL = C::QPL, EPL = C::EPL;
+    int q1off[C::NQP1][QPL], q1mask[C::NQP1][QPL];
+    // P12 lane -> (E2 row, lane item = EPL consecutive x) for pass k
     auto p12_pos = [&](int tid, int k, int& row, int& cq) -> bool {
         const int w = tid / 64 - C::W12, l = tid % 64;
         row = (k * C::NWAVE + w) * C::RPW + l / C::NQ1X;
@@ -607,15 +697,45 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     for (int k = 0; k < C::NQP1; ++k) {
         int row, cq;
         const bool valid = p12_pos(tid0, k, row, cq);
-        const int gx = x0 - 2 * R + EPL * cq, gy = y0 - 2 * R + row;
+#pragma unroll
+        for (int h = 0; h < QPL; ++h) {
+            const int gx = x0 - 2 * R + EPL * cq + 4 * h, gy = y0 - 2 * R + row;
+            int m = 0;
+            if (valid && gy >= 0 && gy < ny) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) m |= (gx + e >= 0 && gx + e < nx) ? (1 << e) : 0;
+            }
+            q1mask[k][h] = m;
+            q1off[k][h] = (EDGE ? valid : m == 0xF) ? (gy * sy + gx) * ESZ : kBadOff;
+        }
+    }
+    // Lc / v5 / output quads: offsets and masks are recomputed at their one use per step
+    // (a few integer ops) rather than held in registers across the march.
+    // P3's center slice on the E1 apron, on the quad grid of E2 (first quad starts C::XC
+    // elements left of the E1 apron), so Lc quads are aligned like P1's
+    auto quad_c = [&](int tid, int& off, int& mask) {
+        const int row = tid / C::NQCX, cq = tid % C::NQCX;
+        const int gx = x0 - R - C::XC + 4 * cq, gy = y0 - R + row;
         int m = 0;
-        if (valid && gy >= 0 && gy < ny) {
+        if (tid < C::NQC && gy >= 0 && gy < ny) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) m |= (gx + e >= 0 && gx + e < nx) ? (1 << e) : 0;
         }
-        q1mask[k] = m;
-        q1off[k] = (EDGE ? valid : m == 0xF) ? (gy * sy + gx) * ESZ : kBadOff;
-    }
+        mask = m;
+        off = (EDGE ? tid < C::NQC : m == 0xF) ? (gy * sy + gx) * ESZ : kBadOff;
+    };
+    auto quad_t = [&](int q, int& ox, int& oy, int& mask) {  // tile quad q: output positions
+        const int row = q / (TX / 4), cq = q % (TX / 4);
+        ox = x0 + 4 * cq;
+        oy = y0 + row;
+        int m = 0;
+        if (q >= 0 && q < C::NQ5 && oy < oy_end) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) m |= (ox + e < ox_end) ? (1 << e) : 0;
+        }
+        mask = m;
+    };
+
     auto load_quad = [&](rsrc_t r, int off, int mask, float (&v)[4]) {
         if constexpr (EDGE) load_quad_masked<TIn>(r, off, mask, v);
         else Quad<TIn>::load(r, off, v);
@@ -634,12 +754,14 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
         for (int z = za; z <= zb_; ++z) {
             const rsrc_t rs = slice_rsrc(z);
 #pragma unroll
-            for (int k = 0; k < C::NQP1; ++k) {
-                float v[4];
-                load_quad(rs, q1off[k], q1mask[k], v);
+            for (int k = 0; k < C::NQP1; ++k)
 #pragma unroll
-                for (int e = 0; e < 4; ++e) zv[k][e] += (double)v[e];
-            }
+                for (int h = 0; h < QPL; ++h) {
+                    float v[4];
+                    load_quad(rs, q1off[k][h], q1mask[k][h], v);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) zv[k][4 * h + e] += (double)v[e];
+                }
         }
     }
 
@@ -651,29 +773,48 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
 #pragma unroll
     for (int j = 0; j < K5; ++j) pre[j] = (f2){0.0f, 0.0f};
 
+    // P3 item of a thread (-1: none). GF_P3_SPREAD: the items spread evenly over all waves
+    // (every wave carries the same P3 work, so no SIMD finishes its share late), else the top
+    // N3 threads.
+    auto p3_item = [&](int tid) -> int {
+        if constexpr (GF_P3_SPREAD) {
+            constexpr int per = (C::N3 + C::NWAVE - 1) / C::NWAVE;
+            const int l = tid % 64, it = (tid / 64) * per + l;
+            return (l < per && it < C::N3) ? it : -1;
+        } else {
+            return tid - C::T3;
+        }
+    };
     // ---- phase bodies ----------------------------------------------------------------------
     float pa[C::NQP1][EPL], ps[C::NQP1][EPL];  // P1 inputs of the next stage-1 slice (prefetched)
-    float vc[C::K3];  // v of the next P3 slice at this thread's item (prefetched)
-    float v5[K5];     // v of the next P5 output slice at this thread's outputs
+    float vc[C::K3];  // GF_DIRECT: v of the next P3 slice at this thread's item (prefetched)
+    float v5[K5];     // GF_DIRECT: v of the next P5 output slice at this thread's outputs
 #pragma unroll
     for (int j = 0; j < K5; ++j) v5[j] = 0.0f;
     auto load_p1 = [&](rsrc_t ra, rsrc_t rs) {  // entering slice zc+R, leaving slice zc-R-1
 #pragma unroll
-        for (int k = 0; k < C::NQP1; ++k) {
-            float a4[4], s4[4];
-            load_quad(ra, q1off[k], q1mask[k], a4);
-            load_quad(rs, q1off[k], q1mask[k], s4);
+        for (int k = 0; k < C::NQP1; ++k)
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                pa[k][e] = a4[e];
-                ps[k][e] = s4[e];
+            for (int h = 0; h < QPL; ++h) {
+                float a4[4], s4[4];
+                if constexpr (ABL & 8) { for (int e = 0; e < 4; ++e) a4[e] = 1.0f; }
+                else load_quad(ra, q1off[k][h], q1mask[k][h], a4);
+                if constexpr (ABL & 1) { for (int e = 0; e < 4; ++e) s4[e] = 0.5f; }
+                else if constexpr (!EDGE && GF_LEAVE_AUX != 0)
+                    Quad<TIn>::template load<GF_LEAVE_AUX>(rs, q1off[k][h], s4);
+                else load_quad(rs, q1off[k][h], q1mask[k][h], s4);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    pa[k][4 * h + e] = a4[e];
+                    ps[k][4 * h + e] = s4[e];
+                }
             }
-        }
     };
     // P12: z-window of v (f64, running) and its x-window sums on the E2 apron -> Hx. The x
     // neighbours come from the adjacent lanes' quads by DPP wave shifts (whole rows per wave),
     // so the z-window never goes through LDS.
     auto do_p12 = [&](int tid) {
+        if constexpr (ABL & 1024) return;
 #pragma unroll
         for (int k = 0; k < C::NQP1; ++k) {
             int row, cq;
@@ -692,8 +833,13 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
             for (int n = 1; n <= NB; ++n)
 #pragma unroll
                 for (int e = 0; e < EPL; ++e) {
-                    win[EPL * (NB - n) + e] = dpp_from_lower(win[EPL * (NB - n + 1) + e]);
-                    win[EPL * (NB + n) + e] = dpp_from_upper(win[EPL * (NB + n - 1) + e]);
+                    if constexpr (ABL & 512) {
+                        win[EPL * (NB - n) + e] = win[EPL * (NB - n + 1) + e] * 0.5;
+                        win[EPL * (NB + n) + e] = win[EPL * (NB + n - 1) + e] * 0.25;
+                    } else {
+                        win[EPL * (NB - n) + e] = dpp_from_lower(win[EPL * (NB - n + 1) + e]);
+                        win[EPL * (NB + n) + e] = dpp_from_upper(win[EPL * (NB + n - 1) + e]);
+                    }
                 }
             double vin[EPL + 2 * R], hs[EPL];
 #pragma unroll
@@ -718,102 +864,143 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
             }
         }
     };
-    // Pointwise stage on NP pairs of E1 positions, packed (both lanes of every op in one issue):
+    // Pointwise stage on NP pairs of E1 positions, packed (both lanes of every op in one issue)
+    // and written op-by-op across the pairs so dependent packed ops are interleaved (gfx950
+    // needs an s_nop between back-to-back dependent v_pk_* otherwise):
     //   u = RN(RN(U) / c)   (summed_area_table_mean, exact: Markstein with rcp = RN(1/c))
     //   s = (v - u)^2;  a = s / (s + eps);  b = (1 - a) * u          (guided_filter.rs:126-137)
     constexpr int NP3 = C::K3 / 2;
+    // The compiler schedules the pairs as separate chains, each dependent v_pk_* then waiting on
+    // an s_nop; a scheduling fence after every op keeps them in lockstep instead (a fence, not
+    // an asm statement: the hazard recognizer pads after inline asm).
+    auto sync = [&](f2 (&)[NP3]) {
+        if constexpr (GF_PW_SYNC) __builtin_amdgcn_sched_barrier(0);
+    };
     auto pointwise = [&](const f2 (&Uf)[NP3], const f2 (&v)[NP3], const f2 (&fc)[NP3],
                          const f2 (&rc)[NP3], f2 (&a)[NP3], f2 (&bb)[NP3]) {
         f2 q[NP3], r[NP3], u[NP3], sq[NP3], den[NP3], y[NP3], e[NP3];
 #pragma unroll
         for (int k = 0; k < NP3; ++k) q[k] = Uf[k] * rc[k];
+        sync(q);
 #pragma unroll
         for (int k = 0; k < NP3; ++k) r[k] = pk_fma(-q[k], fc[k], Uf[k]);
+        sync(r);
 #pragma unroll
         for (int k = 0; k < NP3; ++k) u[k] = pk_fma(r[k], rc[k], q[k]);
+        sync(u);
 #pragma unroll
         for (int k = 0; k < NP3; ++k) sq[k] = v[k] - u[k];
+        sync(sq);
 #pragma unroll
         for (int k = 0; k < NP3; ++k) sq[k] = sq[k] * sq[k];  // (v - u).powf(2.0)
+        sync(sq);
+        if constexpr (ABL & 32) {
 #pragma unroll
-        for (int k = 0; k < NP3; ++k) den[k] = sq[k] + (f2){eps, eps};
+            for (int k = 0; k < NP3; ++k) { a[k] = sq[k]; bb[k] = u[k]; }
+        } else {
 #pragma unroll
-        for (int k = 0; k < NP3; ++k)
-            y[k] = (f2){__builtin_amdgcn_rcpf(den[k].x), __builtin_amdgcn_rcpf(den[k].y)};
-        // a = s / (s + eps): Markstein's correction on v_rcp_f32 (within 1 ulp)
+            for (int k = 0; k < NP3; ++k) den[k] = sq[k] + (f2){eps, eps};
+            sync(den);
 #pragma unroll
-        for (int k = 0; k < NP3; ++k) q[k] = sq[k] * y[k];
+            for (int k = 0; k < NP3; ++k)
+                y[k] = (f2){__builtin_amdgcn_rcpf(den[k].x), __builtin_amdgcn_rcpf(den[k].y)};
+            sync(y);
+            if constexpr (GF_NEWTON_A) {  // refine 1/den before Markstein's correction
 #pragma unroll
-        for (int k = 0; k < NP3; ++k) r[k] = pk_fma(-den[k], q[k], sq[k]);
+                for (int k = 0; k < NP3; ++k) e[k] = pk_fma(-den[k], y[k], (f2){1.0f, 1.0f});
 #pragma unroll
-        for (int k = 0; k < NP3; ++k) a[k] = pk_fma(r[k], y[k], q[k]);
+                for (int k = 0; k < NP3; ++k) y[k] = pk_fma(e[k], y[k], y[k]);
+            }
 #pragma unroll
-        for (int k = 0; k < NP3; ++k) e[k] = (f2){1.0f, 1.0f} - a[k];
+            for (int k = 0; k < NP3; ++k) q[k] = sq[k] * y[k];
+            sync(q);
+            if constexpr (GF_A_RCP) {
 #pragma unroll
-        for (int k = 0; k < NP3; ++k) bb[k] = e[k] * u[k];
+                for (int k = 0; k < NP3; ++k) a[k] = q[k];
+            } else {
+#pragma unroll
+                for (int k = 0; k < NP3; ++k) r[k] = pk_fma(-den[k], q[k], sq[k]);
+                sync(r);
+#pragma unroll
+                for (int k = 0; k < NP3; ++k) a[k] = pk_fma(r[k], y[k], q[k]);
+                sync(a);
+            }
+#pragma unroll
+            for (int k = 0; k < NP3; ++k) e[k] = (f2){1.0f, 1.0f} - a[k];
+            sync(e);
+#pragma unroll
+            for (int k = 0; k < NP3; ++k) bb[k] = e[k] * u[k];
+        }
     };
     static_assert(C::K3 % 2 == 0, "P3 works on pairs");
     // every P3 segment lies inside the apron: unconditional Lab stores (a guard lets the compiler
     // sink the second pair's pointwise chain into it, serialising the pairs)
     constexpr bool kRowsWhole = C::E1Y % C::K3 == 0;
     auto do_p3 = [&](int tid, int zc) {  // y-window (f64) of Hx -> U; a, b -> Lab
-        const int item = tid - C::T3;
+        const int item = p3_item(tid);
         if (item < 0) return;
+        if constexpr (ABL & 2048) return;
         const int col = item % C::E1X, sg = item / C::E1X;
         const double* src = Hx + (sg * C::K3) * C::PH + col;
         double vin[C::K3 + 2 * R], U[C::K3];
 #pragma unroll
-        for (int j = 0; j < C::K3 + 2 * R; ++j) vin[j] = src[j * C::PH];
+        for (int j = 0; j < C::K3 + 2 * R; ++j) {
+            if constexpr (ABL & 256) vin[j] = j == 0 ? src[0] : vin[j - 1] * 1.0001;
+            else vin[j] = src[j * C::PH];
+        }
         slide_sums_f64<R, C::K3>(vin, U);
         f2* lab = reinterpret_cast<f2*>(Lab);
         f2 Uf[NP3], vv[NP3], fc[NP3], rc[NP3], a[NP3], bb[NP3];
+#if GF_DIRECT
 #pragma unroll
         for (int k = 0; k < NP3; ++k) {
             Uf[k] = (f2){(float)U[2 * k], (float)U[2 * k + 1]};
             vv[k] = (f2){vc[2 * k], vc[2 * k + 1]};  // v of slice zc, loaded a half-step ago
         }
-        if constexpr (INTERIOR) {
-            // every E1 point of the tile has the full x and y windows: count = W^2 * cz(zc)
-            // (wave-uniform); planes outside the domain hold no (a, b)
-            const bool zin = (unsigned)zc < (unsigned)nz;
-            const int cnt = W * W * clamped_count(min(max(zc, 0), nz - 1), nz, R);
-            const float fcs = (float)cnt, rcs = rcp_tab[cnt];
+#else
+        const float* vsrc = Lc + (sg * C::K3) * C::PC + C::XC + col;  // v of slice zc (C1)
+#pragma unroll
+        for (int k = 0; k < NP3; ++k) {
+            Uf[k] = (f2){(float)U[2 * k], (float)U[2 * k + 1]};
+            vv[k] = (f2){vsrc[(2 * k) * C::PC], vsrc[(2 * k + 1) * C::PC]};
+        }
+#endif
+        if (xy_interior && zc - R >= 0 && zc + R < nz) {  // wave-uniform: count = W^3
 #pragma unroll
             for (int k = 0; k < NP3; ++k) {
-                fc[k] = (f2){fcs, fcs};
-                rc[k] = (f2){rcs, rcs};
+                fc[k] = (f2){kW3, kW3};
+                rc[k] = (f2){rcp_w3, rcp_w3};
             }
             pointwise(Uf, vv, fc, rc, a, bb);
 #pragma unroll
             for (int k = 0; k < NP3; ++k) {
                 const int ey = sg * C::K3 + 2 * k;
-                const f2 ab0 = zin ? __builtin_shufflevector(a[k], bb[k], 0, 2) : (f2){0.f, 0.f};
-                const f2 ab1 = zin ? __builtin_shufflevector(a[k], bb[k], 1, 3) : (f2){0.f, 0.f};
-                if (kRowsWhole || ey < C::E1Y) lab[ey * C::PA + col] = ab0;
-                if (kRowsWhole || ey + 1 < C::E1Y) lab[(ey + 1) * C::PA + col] = ab1;
-            }
-        } else {
-            const int gx = x0 - R + col;
-            const bool xzin = gx >= 0 && gx < nx && zc >= 0 && zc < nz;
-            const int cxz = clamped_count(gx, nx, R) * clamped_count(zc, nz, R);
-#pragma unroll
-            for (int k = 0; k < NP3; ++k) {
-                const int gy = y0 - R + sg * C::K3 + 2 * k;
-                const int c0 = clamped_count(gy, ny, R) * cxz, c1 = clamped_count(gy + 1, ny, R) * cxz;
-                fc[k] = (f2){(float)c0, (float)c1};
-                rc[k] = (f2){rcp_tab[c0], rcp_tab[c1]};
-            }
-            pointwise(Uf, vv, fc, rc, a, bb);
-#pragma unroll
-            for (int k = 0; k < NP3; ++k) {
-                const int ey = sg * C::K3 + 2 * k;
-                const int gy = y0 - R + ey;
-                // zero outside the domain: the clamped window sums of stage 2
-                const bool ok0 = xzin && gy >= 0 && gy < ny, ok1 = xzin && gy + 1 >= 0 && gy + 1 < ny;
-                if (kRowsWhole || ey < C::E1Y) lab[ey * C::PA + col] = ok0 ? (f2){a[k].x, bb[k].x} : (f2){0.f, 0.f};
+                if (kRowsWhole || ey < C::E1Y) lab[ey * C::PA + col] = __builtin_shufflevector(a[k], bb[k], 0, 2);
                 if (kRowsWhole || ey + 1 < C::E1Y)
-                    lab[(ey + 1) * C::PA + col] = ok1 ? (f2){a[k].y, bb[k].y} : (f2){0.f, 0.f};
+                    lab[(ey + 1) * C::PA + col] = __builtin_shufflevector(a[k], bb[k], 1, 3);
             }
+            return;
+        }
+        const int gx = x0 - R + col;
+        const bool xzin = gx >= 0 && gx < nx && zc >= 0 && zc < nz;
+        const int cxz = clamped_count(gx, nx, R) * clamped_count(zc, nz, R);
+#pragma unroll
+        for (int k = 0; k < NP3; ++k) {
+            const int gy = y0 - R + sg * C::K3 + 2 * k;
+            const int c0 = clamped_count(gy, ny, R) * cxz, c1 = clamped_count(gy + 1, ny, R) * cxz;
+            fc[k] = (f2){(float)c0, (float)c1};
+            rc[k] = (f2){rcp_tab[c0], rcp_tab[c1]};
+        }
+        pointwise(Uf, vv, fc, rc, a, bb);
+#pragma unroll
+        for (int k = 0; k < NP3; ++k) {
+            const int ey = sg * C::K3 + 2 * k;
+            const int gy = y0 - R + ey;
+            // zero outside the domain: the clamped window sums of stage 2
+            const bool ok0 = xzin && gy >= 0 && gy < ny, ok1 = xzin && gy + 1 >= 0 && gy + 1 < ny;
+            if (kRowsWhole || ey < C::E1Y) lab[ey * C::PA + col] = ok0 ? (f2){a[k].x, bb[k].x} : (f2){0.f, 0.f};
+            if (kRowsWhole || ey + 1 < C::E1Y)
+                lab[(ey + 1) * C::PA + col] = ok1 ? (f2){a[k].y, bb[k].y} : (f2){0.f, 0.f};
         }
     };
     auto do_p4 = [&](int tid) {  // x-window sums of (a, b) rows -> Hab
@@ -824,12 +1011,16 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
         if (__builtin_amdgcn_readfirstlane(tid >> 6) * 64 >= C::N4) return;
 #endif
         if (item >= C::N4) return;
+        if constexpr (ABL & 4096) return;
         const int row = item % C::E1Y, sg = item / C::E1Y;
         const float4* src = reinterpret_cast<const float4*>(Lab + row * C::PA + sg * C::K4);
         f2 vin[C::K4 + 2 * R], vout[C::K4];
+        float4 f0 = src[0];
 #pragma unroll
         for (int j = 0; j < (C::K4 + 2 * R) / 2; ++j) {
-            const float4 f = src[j];
+            float4 f;
+            if constexpr (ABL & 128) { f = f0; f0.x *= 1.0001f; f0.y *= 0.999f; f0.z *= 1.001f; f0.w *= 0.9999f; }
+            else f = src[j];
             vin[2 * j] = (f2){f.x, f.y};
             vin[2 * j + 1] = (f2){f.z, f.w};
         }
@@ -849,13 +1040,17 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     // slice, when it is turned into the suffix sum over [P, W) in place; a window ending at
     // position P of block B+1 is suffix_B(P+1) + prefix_{B+1}(P). ~3 packed adds per output
     // instead of an f64 running sum (10 ops).
-    rsrc_t ro5;  // the output slice P5 stores to this step
-    auto do_p5 = [&](int tid, int zc, auto slot_c) {  // y-window -> slice sums; z; out -> global
+    rsrc_t ro5;  // GF_DIRECT: the output slice P5 stores to this step
+    auto do_p5 = [&](int tid, int zc, auto slot_c) {  // y-window -> slice sums; z; out -> Lout
+        if constexpr (ABL & 8192) return;
         const int col5 = tid % TX, seg5 = tid / TX;
         const f2* src = reinterpret_cast<const f2*>(Hab) + (seg5 * K5) * C::PB + col5;
         f2 vin[K5 + 2 * R], s2[K5];
 #pragma unroll
-        for (int j = 0; j < K5 + 2 * R; ++j) vin[j] = src[j * C::PB];
+        for (int j = 0; j < K5 + 2 * R; ++j) {
+            if constexpr (ABL & 64) vin[j] = j == 0 ? src[0] : vin[j - 1] * (f2){1.0001f, 0.999f};
+            else vin[j] = src[j * C::PB];
+        }
         core_window_sums<R, K5>(vin, s2);
         constexpr int P = decltype(slot_c)::value;
         f2 AB[K5];
@@ -873,46 +1068,87 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
                 for (int j = 0; j < K5; ++j) ring[q][j] = ring[q][j] + ring[q + 1][j];
         }
         const int zo = zc - R;
+#if !GF_DIRECT
+        if (zo < zo_begin || zo >= zo_end) return;  // wave-uniform
+#endif
         const int ox = x0 + col5, oyb = y0 + seg5 * K5;
-        // steps that emit nothing run too, their stores dropped by the descriptor; the z count
-        // is clamped so its table index stays valid there
+        const bool interior = xy_interior && zo - R >= 0 && zo + R < nz;  // wave-uniform
+        // (GF_DIRECT: steps that emit nothing run too, their stores dropped by the descriptor;
+        //  the z count is clamped so its table index stays valid there)
         const int zq = min(max(zo, 0), nz - 1);
-        f2 rc[K5];
-        if constexpr (INTERIOR) {
-            const float r = rcp_tab[W * W * clamped_count(zq, nz, R)];  // wave-uniform
-#pragma unroll
-            for (int j = 0; j < K5; ++j) rc[j] = (f2){r, r};
-        } else {
-            const int cxz = clamped_count(ox, nx, R) * clamped_count(zq, nz, R);
-#pragma unroll
-            for (int j = 0; j < K5; ++j) {
-                const float r = rcp_tab[clamped_count(oyb + j, ny, R) * cxz];
-                rc[j] = (f2){r, r};
-            }
-        }
-        // (sum as f32) * RN(1/count) for a and b together: the stage-2 means (one multiply; the
-        // f32 sums already differ from the reference's f64 SAT sums by a few ulp)
+        const int cxz = interior ? 0 : clamped_count(ox, nx, R) * clamped_count(zq, nz, R);
+        f2 fc[K5], rc[K5], q[K5], r[K5];
 #pragma unroll
         for (int j = 0; j < K5; ++j) {
-            const f2 q = AB[j] * rc[j];
+            if (interior) {
+                fc[j] = (f2){kW3, kW3};
+                rc[j] = (f2){rcp_w3, rcp_w3};
+            } else {
+                const int cnt = clamped_count(oyb + j, ny, R) * cxz;
+                const float f = (float)cnt, rr = rcp_tab[cnt];
+                fc[j] = (f2){f, f};
+                rc[j] = (f2){rr, rr};
+            }
+        }
+        // (sum as f32) / (count as f32) for a and b together
+#pragma unroll
+        for (int j = 0; j < K5; ++j) q[j] = AB[j] * rc[j];
+        if constexpr (!GF_FASTDIV5) {  // correctly rounded (Markstein)
+#pragma unroll
+            for (int j = 0; j < K5; ++j) r[j] = pk_fma(-q[j], fc[j], AB[j]);
+#pragma unroll
+            for (int j = 0; j < K5; ++j) q[j] = pk_fma(r[j], rc[j], q[j]);
+        }
+#if GF_DIRECT
+        (void)r;
+#pragma unroll
+        for (int j = 0; j < K5; ++j) {
             const int oy = oyb + j;
-            const float o = __fadd_rn(__fmul_rn(v5[j], q.x), q.y);  // v*=ma; v+=mb
+            const float o = __fadd_rn(__fmul_rn(v5[j], q[j].x), q[j].y);  // v*=ma; v+=mb
             const int off = (ox < ox_end && oy < oy_end)
                                 ? ((oy - p.oy0) * osy + (ox - p.ox0)) * OSZ : kBadOff;
             Buf<TOut>::store(from_f32<TOut>(o), ro5, opaque(off));
         }
+#else
+#pragma unroll
+        for (int j = 0; j < K5; ++j) {
+            const int ty = seg5 * K5 + j;
+            const float v = Lv5[ty * TX + col5];                  // v of slice zo (staged in C1)
+            Lout[ty * TX + col5] = __fadd_rn(__fmul_rn(v, q[j].x), q[j].y);  // v*=ma; v+=mb
+        }
+#endif
     };
 
-    // ---- v loaders: one element per access, lanes on consecutive x (coalesced rows) -------------
+    // ---- C1 staging: 16-byte quads between global memory and the LDS tiles ------------------
     // Every global access of the march below is unconditional, in the same order every step:
     // out-of-range slices, inactive lanes and non-emitting steps use null descriptors or
     // kBadOff instead of branches. Branches around memory instructions make the compiler's
     // vmcnt accounting fall back to draining the loads just issued (measured: a 1.6x slower
     // kernel); straight-line, it waits for exactly the step-old load it needs.
+    float cq4[4], vq4[4];  // v of the next Lc slice / the next Lv5 slice (prefetched a step ahead)
+    auto load_c = [&](rsrc_t r) {
+        if constexpr (ABL & 2) { for (int e = 0; e < 4; ++e) cq4[e] = 1.0f; }
+        else {
+            int off, mask;
+            quad_c((int)threadIdx.x, off, mask);
+            load_quad(r, off, mask, cq4);
+        }
+    };
+    auto load_v5 = [&](rsrc_t r) {
+        if constexpr (ABL & 4) { for (int e = 0; e < 4; ++e) vq4[e] = 1.0f; }
+        else {
+            const int q = (int)threadIdx.x - (NT - C::NQ5);
+            int ox, oy, mask;
+            quad_t(q, ox, oy, mask);
+            const int off = (EDGE ? q >= 0 : mask == 0xF) ? (oy * sy + ox) * ESZ : kBadOff;
+            load_quad(r, off, mask, vq4);
+        }
+    };
+    // GF_DIRECT loaders: one element per access, lanes on consecutive x (coalesced rows).
     // Positions outside the domain either read 0 through the range check or read a neighbour
     // row's value that is never used (P3 zeroes its out-of-domain (a, b); P5's store drops).
     auto load_p3v = [&](rsrc_t r) {
-        const int item = (int)threadIdx.x - C::T3;
+        const int item = p3_item((int)threadIdx.x);
         const int col = item % C::E1X, sg = item / C::E1X;
         const int gx = x0 - R + col, gy0 = y0 - R + sg * C::K3;
 #pragma unroll
@@ -930,26 +1166,59 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
         for (int j = 0; j < K5; ++j) {
             const int oy = oyb + j;
             const bool ok = ox < ox_end && oy < oy_end;
-            v5[j] = Buf<TIn>::load(r, opaque(ok ? (oy * sy + ox) * ESZ : kBadOff));
+            v5[j] = Buf<TIn>::template load<GF_V5_AUX>(r, opaque(ok ? (oy * sy + ox) * ESZ : kBadOff));
         }
     };
+    float* const dummy = reinterpret_cast<float*>(smem + C::OFF_DUMMY);  // inactive lanes' writes
+    auto write_c = [&](int tid) {
+        const int row = tid / C::NQCX, cq = tid % C::NQCX;
+        float* dst = tid < C::NQC ? Lc + row * C::PC + 4 * cq : dummy;
+        *reinterpret_cast<float4*>(dst) = make_float4(cq4[0], cq4[1], cq4[2], cq4[3]);
+    };
+    auto write_v5 = [&](int tid) {
+        const int q = tid - (NT - C::NQ5);
+        const int row = q / (TX / 4), cq = q % (TX / 4);
+        float* dst = q >= 0 ? Lv5 + row * TX + 4 * cq : dummy;
+        *reinterpret_cast<float4*>(dst) = make_float4(vq4[0], vq4[1], vq4[2], vq4[3]);
+    };
+    auto store_out = [&](int tid, rsrc_t ro) {  // Lout -> global, one quad per thread
+        const bool act = tid < C::NQ5;
+        const int row = act ? tid / (TX / 4) : 0, cq = act ? tid % (TX / 4) : 0;
+        const float4 o4 = *reinterpret_cast<const float4*>(Lout + row * TX + 4 * cq);
+        const float o[4] = {o4.x, o4.y, o4.z, o4.w};
+        int ox, oy, mask;
+        quad_t(tid, ox, oy, mask);
+        const int off =
+            (EDGE ? act : mask == 0xF) ? ((oy - p.oy0) * osy + (ox - p.ox0)) * OSZ : kBadOff;
+        if constexpr (EDGE) store_quad_masked<TOut>(o, ro, off, mask);
+        else Quad<TOut>::store(o, ro, off);
+    };
 
-    // ---- prologue: stage 1 of the first slice up to Hx; prefetch step 1 ---------------------
+    // ---- prologue: stage 1 of the first slice up to Hx, first Lc; prefetch step 1 -----------
     load_p1(slice_rsrc(zc_begin + R), slice_rsrc(zc_begin - R - 1));
+#if GF_DIRECT
     load_p3v(slice_rsrc(zc_begin));
+    if constexpr (C::ONEBAR) set_hx(zc_begin);
     do_p12(tid0);
+#else
+    load_c(slice_rsrc(zc_begin));
+    do_p12(tid0);
+    write_c(tid0);
+    load_c(slice_rsrc(zc_begin + 1));
+    load_v5(slice_rsrc(zc_begin - R));
+#endif
     load_p1(slice_rsrc(zc_begin + 1 + R), slice_rsrc(zc_begin - R));
-    lds_barrier();
+    lds_barrier_abl<ABL>();
 
     // ---- slice streams: descriptors advanced by one slice per step (two 32-bit adds each)
     //      instead of rebuilt from z (a 64-bit multiply and range checks per descriptor) ------
-    // step i reads slice zb = i+1-R (leaving slice of P1(i+2), and v5), zb+R+1 = i+2 (P3's v)
-    // and zb+2R+1 = i+2+R (entering slice of P1(i+2)); it stores output slice zs = i-1-R.
+    // step i reads slice zb = i+1-R (leaving slice of P1(i+2), and v5), zb+R+1 = i+2 (Lc) and
+    // zb+2R+1 = i+2+R (entering slice of P1(i+2)); it stores output slice zs = i-1-R.
     const int64_t sstride = p.in_sz * ESZ, osstride = p.out_sz * OSZ;
-    const int64_t off_a = (int64_t)(2 * R + 1) * sstride;
+    const int64_t off_c = (int64_t)(R + 1) * sstride, off_a = (int64_t)(2 * R + 1) * sstride;
     int zb = zc_begin + 1 - R;
     int64_t ob = (int64_t)(zb - p.in_z0) * sstride;
-    int zs = zc_begin - 1 - R;  // output slice of this step's P5
+    int zs = zc_begin - (C::ONEBAR ? 2 : 1) - R;  // output slice of this step's P5
     int64_t os = (int64_t)(zs - p.oz0) * osstride;
     const char* out_base = static_cast<const char*>(p.out);
     const unsigned nzo = (unsigned)(zo_end - zo_begin);
@@ -958,43 +1227,108 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     };
 
     // ---- pipelined march, unrolled by W so the ring slot of every P5 is a constant ----------
-    // Iteration i runs
-    //   C0: P3(i) [U -> a,b on the E1 apron] + P5(i-1) [y-sums, z-blocks, out(i-1-R)]
-    //   C1: the loads of the next step, P12(i+1) [z-window of v, x-sums], P4(i) [x-sums of (a,b)]
-    // with separate LDS buffers per hand-off, so each barrier interval holds independent work
-    // from different slices. The step count is padded to a multiple of W, at least one past the
-    // last stage-1 slice so that P5 / the store of the last output slice happen inside the loop:
-    // no guards inside. Padded steps emit nothing (zo >= zo_end).
-    const int n_steps = (zc_end - zc_begin + 1 + W - 1) / W * W;
+    // The step count is padded to a multiple of W, at least one past the last stage-1 slice so
+    // that P5/the store of the last output slice happen inside the loop: no guards inside.
+    // Padded steps emit nothing (zo >= zo_end).
+    // (ONEBAR: P5 runs two steps behind P3, so one more step.)
+    const int n_steps = (zc_end - zc_begin + (C::ONEBAR ? 2 : 1) + W - 1) / W * W;
     for (int i0 = zc_begin; i0 < zc_begin + n_steps; i0 += W) {
         static_for<0, W>([&](auto kc) {
             constexpr int k = decltype(kc)::value;
             const int i = i0 + k;
             const int tid = threadIdx.x;
             const rsrc_t r_b = rs_in(ob, zb);
+            if constexpr (C::ONEBAR) {
+                // One barrier per step. Step i: P12(i+1) -> Hx[i+1], P5(i-2) <- Hab[i],
+                // P3(i) <- Hx[i] -> Lab[i], P4(i-1) <- Lab[i-1] -> Hab[i-1] (buffers by parity:
+                // each is written in one step and read in the next). The first steps' P4/P5
+                // work on unwritten buffers for slices that lie in no emitted window (see the
+                // GF_DIRECT note on P5); their stores go to zero-record descriptors.
+                ro5 = make_rsrc(out_base + os,
+                                (unsigned)(zs - zo_begin) < nzo ? oslice_bytes : 0u);
+                if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(3);
+                set_hx(i + 1);
+                do_p12(tid);
+                load_p1(rs_in(ob + off_a, zb + 2 * R + 1), r_b);  // for P12(i+2)
+                if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(1);
+                set_hab(i);
+                do_p5(tid, i - 2, std::integral_constant<int, (k + 2 * W - 2) % W>{});
+                load_p5v(rs_in(ob - 2 * sstride, zb - 2));  // slice i-1-R, for P5(i-1)
+                set_hx(i);
+                set_lab(i);
+                do_p3(tid, i);
+                load_p3v(rs_in(ob + (int64_t)R * sstride, zb + R));  // slice i+1, for P3(i+1)
+                set_lab(i - 1);
+                set_hab(i - 1);
+                do_p4(tid);
+                lds_barrier_abl<ABL>();
+                ++zb;
+                ob += sstride;
+                ++zs;
+                os += osstride;
+                return;
+            }
+            // tools/ instrumentation only (ABL & 16384): per-wave stamps of one workgroup
+            auto stamp = [&](int slot) {
+                if constexpr (ABL & 16384) {
+                    const int st = i - zc_begin - 64;
+                    if ((int)blockIdx.x == p.trace_block && st >= 0 && st < 18 &&
+                        (threadIdx.x & 63) == 0)
+                        p.trace[(st * 16 + threadIdx.x / 64) * 8 + slot] =
+                            __builtin_amdgcn_s_memtime();
+                }
+            };
+#if GF_DIRECT
             ro5 = make_rsrc(out_base + os, (unsigned)(zs - zo_begin) < nzo ? oslice_bytes : 0u);
+#endif
+            stamp(0);
             // Fair progress across the waves of a SIMD: the hardware issues oldest-first, which
             // staggers the waves so the youngest runs its last phase alone, latency exposed. A
             // wave drops its priority as it completes a phase, so laggards catch up.
             if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(3);
-            // C0: P3(i) + P5(i-1) (LDS and registers only). P5 runs unconditionally, so no
-            // branch separates its stores from the loads waited on later (the first call's slice
-            // lies in no emitted window, and its stores go to a zero-record descriptor)
-            do_p3(tid, i);
-            if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(1);
-            do_p5(tid, i - 1, std::integral_constant<int, (k + W - 1) % W>{});
-            lds_barrier();
+            // C0: P3(i) + P5(i-1) (LDS and registers only)
+            if constexpr (C::ORDER & 1) {
+                if (i > zc_begin) do_p5(tid, i - 1, std::integral_constant<int, (k + W - 1) % W>{});
+                if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(1);
+                do_p3(tid, i);
+            } else {
+                do_p3(tid, i);
+                if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(1);
+                stamp(4);
+                // GF_DIRECT: unconditional, so no branch separates P5's stores from the loads
+                // waited on later (the first call's slice lies in no emitted window, and its
+                // stores go to a zero-record descriptor)
+                if (GF_DIRECT || i > zc_begin)
+                    do_p5(tid, i - 1, std::integral_constant<int, (k + W - 1) % W>{});
+            }
+            stamp(1);
+            lds_barrier_abl<ABL>();
+            stamp(2);
             if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(3);
-            // C1: the loads of the next step, P12(i+1), P4(i). Every wait here is for a load
-            // issued a step ago.
-            load_p3v(rs_in(ob + (int64_t)R * sstride, zb + R));  // P3 slice i+1
-            load_p5v(rs_in(ob - sstride, zb - 1));                // P5 slice i-R
+            // C1: staging (store out(i-1-R), Lc <- slice i+1, Lv5 <- slice i-R), the loads of
+            // the next step, P12(i+1), P4(i). Every wait here is for a load issued a step ago.
+#if GF_DIRECT
+            // next step's P3 slice i+1 (= zb + R) and P5 slice i-R (= zb - 1)
+            load_p3v(rs_in(ob + (int64_t)R * sstride, zb + R));
+            load_p5v(rs_in(ob - sstride, zb - 1));
+#else
+            store_out(tid, make_rsrc(out_base + os,
+                                     (unsigned)(zs - zo_begin) < nzo ? oslice_bytes : 0u));
+            write_c(tid);
+            write_v5(tid);
+            load_c(rs_in(ob + off_c, zb + R + 1));
+            load_v5(r_b);
+#endif
+            stamp(6);
+            if constexpr (GF_PRIO >= 2) __builtin_amdgcn_s_setprio(2);
             if constexpr (C::ORDER & 2) do_p4(tid);
             do_p12(tid);
             load_p1(rs_in(ob + off_a, zb + 2 * R + 1), r_b);
             if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(1);
+            stamp(5);
             if constexpr (!(C::ORDER & 2)) do_p4(tid);
-            lds_barrier();
+            stamp(3);
+            lds_barrier_abl<ABL>();
             ++zb;
             ob += sstride;
             ++zs;
@@ -1041,11 +1375,11 @@ inline hipError_t allow_dynamic_lds(const void* kern, int bytes, std::atomic<uin
     return hipSuccess;
 }
 
-template <int R, int TY, int NT, typename TIn, typename TOut, int MODE>
+template <int R, int TY, int NT, typename TIn, typename TOut, bool EDGE, int ABL = 0>
 inline hipError_t launch_fused_variant(const GFParams& p, long long nwg, hipStream_t stream) {
     using C = GFConfig<R, TY, NT>;
     const size_t lds = (size_t)C::LDS_BYTES;
-    auto kern = gf3d_fused_kernel<R, TY, NT, TIn, TOut, MODE>;
+    auto kern = gf3d_fused_kernel<R, TY, NT, TIn, TOut, EDGE, ABL>;
     if (hipError_t e = allow_dynamic_lds((const void*)kern, (int)lds, attr_devices<decltype(kern)>()))
         return e;
     if (nwg <= 0) return hipSuccess;
@@ -1054,7 +1388,7 @@ inline hipError_t launch_fused_variant(const GFParams& p, long long nwg, hipStre
     return hipGetLastError();
 }
 
-template <int R, int TY, int NT, typename TIn, typename TOut>
+template <int R, int TY, int NT, typename TIn, typename TOut, int ABL = 0>
 inline hipError_t launch_fused_cfg(const GFParams& p0, hipStream_t stream) {
     using C = GFConfig<R, TY, NT>;
     GFParams p = p0;
@@ -1066,26 +1400,29 @@ inline hipError_t launch_fused_cfg(const GFParams& p0, hipStream_t stream) {
     p.tiles_x = (p.onx + C::TX - 1) / C::TX;
     p.tiles_y = (p.ony + TY - 1) / TY;
     p.nseg = (p.onz + p.zseg - 1) / p.zseg;
-    // Interior tiles (mode 0): the whole E2 apron inside the domain, the tile inside the output
-    // box. Quad-aligned geometry (every quad starts at a multiple of 4 elements: the E2 apron at
-    // x0 - 2R, the output tile at x0; the domain / output box widths multiples of 4): no quad
-    // straddles a boundary, so the other tiles take the unmasked mode 1, else the masked mode 2.
+    // Quad-aligned geometry: every quad starts at a multiple of 4 elements (the E2 apron at
+    // x0 - 2R, the output tile at x0), and the domain / output box widths are multiples of 4,
+    // so no quad straddles a boundary: the first kernel takes every tile.
     const bool quad_ok = (p.ox0 % 4 == 0) && (R % 2 == 0) && (p.nx % 4 == 0) &&
                          (p.onx % 4 == 0) && (p.in_sy % 4 == 0) && (p.in_sz % 4 == 0) &&
                          (p.out_sy % 4 == 0) && (p.out_sz % 4 == 0) &&
                          ((uintptr_t)p.in % (4 * sizeof(TIn)) == 0) &&
                          ((uintptr_t)p.out % (4 * sizeof(TOut)) == 0);
-    interior_tiles(p.ox0, p.ox0 + p.onx, p.nx, C::TX, R, 0, p.tiles_x, p.itx0, p.itx1);
-    interior_tiles(p.oy0, p.oy0 + p.ony, p.ny, TY, R, 0, p.tiles_y, p.ity0, p.ity1);
+    if (quad_ok) {
+        p.itx0 = 0; p.itx1 = p.tiles_x;
+        p.ity0 = 0; p.ity1 = p.tiles_y;
+    } else {
+        // +4 elements of x slack: the last Lc quad of a row may overhang the E1 apron
+        interior_tiles(p.ox0, p.ox0 + p.onx, p.nx, C::TX, R, 4, p.tiles_x, p.itx0, p.itx1);
+        interior_tiles(p.oy0, p.oy0 + p.ony, p.ny, TY, R, 0, p.tiles_y, p.ity0, p.ity1);
+    }
     const long long n_int = (long long)(p.itx1 - p.itx0) * (p.ity1 - p.ity0);
     const long long n_all = (long long)p.tiles_x * p.tiles_y;
     hipError_t e = hipSuccess;
     if (n_int > 0)
-        e = launch_fused_variant<R, TY, NT, TIn, TOut, 0>(p, n_int * p.nseg, stream);
-    if (e == hipSuccess && n_all > n_int) {
-        if (quad_ok) e = launch_fused_variant<R, TY, NT, TIn, TOut, 1>(p, n_all * p.nseg, stream);
-        else e = launch_fused_variant<R, TY, NT, TIn, TOut, 2>(p, n_all * p.nseg, stream);
-    }
+        e = launch_fused_variant<R, TY, NT, TIn, TOut, false, ABL>(p, n_int * p.nseg, stream);
+    if (e == hipSuccess && n_all > n_int)
+        e = launch_fused_variant<R, TY, NT, TIn, TOut, true, ABL>(p, n_all * p.nseg, stream);
     return e;
 }
 

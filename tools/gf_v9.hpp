@@ -33,7 +33,7 @@
 
 #include <cstdlib>
 
-#include "../zarrs_tools_amd/csrc/gf_fused.hpp"
+#include "gf_fused_variants.hpp"
 
 #ifndef GF_V9_K3
 #define GF_V9_K3 2

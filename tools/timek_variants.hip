@@ -1,4 +1,4 @@
-// tools/timek.hip — times the fused guided-filter kernel (r=4, f32, N^3, the bench's synthetic
+// tools/timek_variants.hip — timek over the round-2 kernel with its variant switches (gf_fused_variants.hpp): the A/B baseline.
 // step+noise-like input) and prints a checksum of the output, so builds with different
 // compile-time work splits (-DGF_K3=, -DGF_K4=, ...) can be compared (not a product path).
 #include <hip/hip_runtime.h>
@@ -8,9 +8,12 @@
 #include <cstdlib>
 #include <vector>
 
-#include "../zarrs_tools_amd/csrc/gf_fused.hpp"
+#include "gf_fused_variants.hpp"
 
 using namespace zt;
+#ifndef TK_ABL
+#define TK_ABL 0
+#endif
 #ifndef TK_TY
 #define TK_TY 32
 #endif
@@ -45,10 +48,10 @@ int main(int argc, char** argv) {
     hipEvent_t a, b;
     CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
     std::vector<float> t;
-    CK((launch_fused_cfg<TK_R, TK_TY, TK_NT, float, float>(p, s)));
+    CK((launch_fused_cfg<TK_R, TK_TY, TK_NT, float, float, TK_ABL>(p, s)));
     for (int r = 0; r < 5; ++r) {
         CK(hipEventRecord(a, s));
-        CK((launch_fused_cfg<TK_R, TK_TY, TK_NT, float, float>(p, s)));
+        CK((launch_fused_cfg<TK_R, TK_TY, TK_NT, float, float, TK_ABL>(p, s)));
         CK(hipEventRecord(b, s));
         CK(hipEventSynchronize(b));
         float ms; CK(hipEventElapsedTime(&ms, a, b));

@@ -8,7 +8,7 @@
 #include <cstdlib>
 #include <vector>
 
-#include "../zarrs_tools_amd/csrc/gf_fused.hpp"
+#include "gf_fused_variants.hpp"
 
 using namespace zt;
 
