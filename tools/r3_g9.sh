@@ -1,0 +1,9 @@
+#!/bin/bash
+# round 3, GPU call 9: one grid with per-workgroup tile class (tk_one) vs all-mode-1 / all-mode-0
+set -u
+OUT=gpurun_out/r3g9
+mkdir -p $OUT
+for v in base one m1 m0 base one m1 m0; do timeout -k 10 120 tools/tk_$v 2048 $v 512 >> $OUT/tk.txt 2>&1 || exit 1; done
+for v in base one m1 m0; do timeout -k 10 120 tools/tk_$v 1024 ${v}_1024 1024 >> $OUT/tk.txt 2>&1 || exit 1; done
+for v in base_r2 one_r2 m1_r2 base_r2 one_r2 m1_r2; do timeout -k 10 120 tools/tk_$v 2048 ${v}_2048 256 >> $OUT/tk.txt 2>&1 || exit 1; done
+cat $OUT/tk.txt

@@ -1,6 +1,7 @@
 // tools/timeg4.hip — times the fused 4-D guided-filter kernel (g4_fused.hip, r=2, f32,
-// (4, N, N, N)) and prints a checksum, so builds with compile-time ablations (-DG4_ABL=...) can
-// be compared (not a product path). Build: tools/timeg4.sh build NAME "-DFLAGS"...
+// (4, N, N, N)) and prints a checksum, so builds with compile-time geometry flags (-DG4_KX2=...)
+// can be compared (not a product path; the round-2 load ablations, profiles/r02_ab_harness.txt,
+// are no longer in the product source). Build: tools/timeg4.sh build NAME "-DFLAGS"...
 #include "../zarrs_tools_amd/csrc/g4_fused.hip"
 
 #include <algorithm>

@@ -1,6 +1,7 @@
 // tools/timek.hip — times the fused guided-filter kernel (r=4, f32, N^3, the bench's synthetic
 // step+noise-like input) and prints a checksum of the output, so builds with different
-// compile-time work splits (-DGF_K3=, -DGF_K4=, ...) can be compared (not a product path).
+// compile-time work splits (-DGF_K3=, -DGF_K4=, ...) and launch modes (-DTK_LAUNCH=) can be
+// compared (not a product path).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -19,6 +20,11 @@ using namespace zt;
 #endif
 #ifndef TK_NT
 #define TK_NT 1024
+#endif
+
+#ifndef TK_LAUNCH
+#define TK_LAUNCH 0  // 0: launch_fused_cfg; 1: mode 1 over every tile; 2: mode 0 over every tile
+                     // (timing only: the border tiles' output is wrong)
 #endif
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { \
@@ -42,13 +48,30 @@ int main(int argc, char** argv) {
     p.out_sy = n; p.in_z0 = 0; p.zlo = 0; p.zhi = n; p.nz = p.ny = p.nx = n;
     p.oz0 = p.oy0 = p.ox0 = 0; p.onz = p.ony = p.onx = n; p.zseg = (argc > 3 && atoi(argv[3]) > 0) ? atoi(argv[3]) : 256; p.eps = 2500.0f;
     hipStream_t s; CK(hipStreamCreate(&s));
+    auto launch = [&](const GFParams& p0, hipStream_t st) -> hipError_t {
+        if (TK_LAUNCH == 0) return launch_fused_cfg<TK_R, TK_TY, TK_NT, float, float>(p0, st);
+        using C = GFConfig<TK_R, TK_TY, TK_NT>;
+        GFParams q = p0;
+        volatile float one = 1.0f;
+        q.rcp_w3 = one / (float)C::W3;
+        q.tiles_x = (q.onx + C::TX - 1) / C::TX;
+        q.tiles_y = (q.ony + TK_TY - 1) / TK_TY;
+        q.nseg = (q.onz + q.zseg - 1) / q.zseg;
+        const long long nwg = (long long)q.tiles_x * q.tiles_y * q.nseg;
+        if (TK_LAUNCH == 1) {
+            q.itx0 = q.itx1 = q.ity0 = q.ity1 = 0;
+            return launch_fused_variant<TK_R, TK_TY, TK_NT, float, float, 1>(q, nwg, st);
+        }
+        q.itx0 = 0; q.itx1 = q.tiles_x; q.ity0 = 0; q.ity1 = q.tiles_y;
+        return launch_fused_variant<TK_R, TK_TY, TK_NT, float, float, 0>(q, nwg, st);
+    };
     hipEvent_t a, b;
     CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
     std::vector<float> t;
-    CK((launch_fused_cfg<TK_R, TK_TY, TK_NT, float, float>(p, s)));
+    CK(launch(p, s));
     for (int r = 0; r < 5; ++r) {
         CK(hipEventRecord(a, s));
-        CK((launch_fused_cfg<TK_R, TK_TY, TK_NT, float, float>(p, s)));
+        CK(launch(p, s));
         CK(hipEventRecord(b, s));
         CK(hipEventSynchronize(b));
         float ms; CK(hipEventElapsedTime(&ms, a, b));

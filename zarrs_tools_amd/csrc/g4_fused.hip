@@ -35,10 +35,6 @@ namespace zt {
 namespace {
 
 constexpr int kFTX = 64, kFTY = 8, kFTS = 4;  // tile width, height, timepoints per block
-#ifndef G4_ABL
-#define G4_ABL 0  // tools/timeg4 ablations only (1: no leaving-slice loads, 2: no entering-slice
-                  // loads, 8: no S3 / S5 v loads)
-#endif
 #ifndef G4_Q4
 #define G4_Q4 1  // quad loads in S1 where the geometry allows (see g4_fused_kernel)
 #endif
@@ -300,18 +296,12 @@ __global__ __launch_bounds__(G4FConfig<R>::NT) void g4_fused_kernel(G4FParams p)
         for (int t = 0; t < TS; ++t) {
             const rsrc_t rs = slice(t, zc);
 #pragma unroll
-            for (int j = 0; j < C::KY3; ++j) {
-                if constexpr (G4_ABL & 8) v3[t][j] = (float)j;
-                else v3[t][j] = ldb(rs, off3[j]);
-            }
+            for (int j = 0; j < C::KY3; ++j) v3[t][j] = ldb(rs, off3[j]);
         }
     };
     auto load_v5 = [&](int zo) {
 #pragma unroll
-        for (int t = 0; t < TS; ++t) {
-            if constexpr (G4_ABL & 8) v5[t] = (float)t;
-            else v5[t] = ldv(t, zo, off5);
-        }
+        for (int t = 0; t < TS; ++t) v5[t] = ldv(t, zo, off5);
     };
     load_v5(zc_begin - R);
     load_v3(zc_begin);  // S3's v of the first stage-1 slice; later slices a step ahead
@@ -364,10 +354,8 @@ __global__ __launch_bounds__(G4FConfig<R>::NT) void g4_fused_kernel(G4FParams p)
                 const rsrc_t ra = slice(t, zc + 1 + R), rl = slice(t, zc - R);
 #pragma unroll
                 for (int k = 0; k < NPT; ++k) {
-                    if constexpr (G4_ABL & 2) pa[t][k] = pa[t][k] * 0.999f;
-                    else pa[t][k] = ldb(ra, off[k]);
-                    if constexpr (G4_ABL & 1) ps[t][k] = ps[t][k] * 0.998f;
-                    else ps[t][k] = ldb(rl, off[k]);
+                    pa[t][k] = ldb(ra, off[k]);
+                    ps[t][k] = ldb(rl, off[k]);
                 }
             }
             }

@@ -504,11 +504,11 @@ struct GFConfig {
 //   domain and whose output tile lies inside the output box: unmasked 16-byte accesses, and the
 //   window counts depend on z only, so they are computed once per step (wave-uniform) and P3 / P5
 //   carry no per-lane count or zeroing logic and no branch.
-// MODE 1 (quad): every other tile of a quad-aligned geometry (each 4-element quad of a global
-//   access wholly inside or wholly outside the domain / output box): unmasked accesses, the
-//   outside quads through kBadOff, per-lane clamped counts and zeroing.
-// MODE 2 (edge): every other tile otherwise: element-wise masked accesses.
-// The grid of modes 1 and 2 covers all tiles; the interior ones return at once. Separate kernels
+// MODE 1 (quad): every tile of a quad-aligned geometry (each 4-element quad of a global access
+//   wholly inside or wholly outside the domain / output box): unmasked accesses, the outside
+//   quads through kBadOff, per-lane clamped counts and zeroing (one grid: see launch_fused_cfg).
+// MODE 2 (edge): the border tiles otherwise: element-wise masked accesses. Its grid covers all
+//   tiles; the interior ones (mode 0's) return at once. Separate kernels
 // rather than runtime branches keep each march free of control flow around its memory
 // instructions, so the compiler's vmcnt accounting stays exact (a branch there made it drain
 // every load).
@@ -1075,17 +1075,23 @@ inline hipError_t launch_fused_cfg(const GFParams& p0, hipStream_t stream) {
                          (p.out_sy % 4 == 0) && (p.out_sz % 4 == 0) &&
                          ((uintptr_t)p.in % (4 * sizeof(TIn)) == 0) &&
                          ((uintptr_t)p.out % (4 * sizeof(TOut)) == 0);
+    const long long n_all = (long long)p.tiles_x * p.tiles_y;
+    if (quad_ok) {
+        // one grid, every tile in mode 1. Measured at 2048^3 r=4: 30.2 ms, against 35.2 ms for
+        // mode 0 + a second grid of the border tiles (that grid's tail) and 30.4 ms for one grid
+        // choosing the class per workgroup (both marches in one kernel: more SGPR spills); mode 0
+        // alone over every tile (border output wrong, a bound only) 29.1 ms.
+        p.itx0 = p.itx1 = p.ity0 = p.ity1 = 0;
+        return launch_fused_variant<R, TY, NT, TIn, TOut, 1>(p, n_all * p.nseg, stream);
+    }
     interior_tiles(p.ox0, p.ox0 + p.onx, p.nx, C::TX, R, 0, p.tiles_x, p.itx0, p.itx1);
     interior_tiles(p.oy0, p.oy0 + p.ony, p.ny, TY, R, 0, p.tiles_y, p.ity0, p.ity1);
     const long long n_int = (long long)(p.itx1 - p.itx0) * (p.ity1 - p.ity0);
-    const long long n_all = (long long)p.tiles_x * p.tiles_y;
     hipError_t e = hipSuccess;
     if (n_int > 0)
         e = launch_fused_variant<R, TY, NT, TIn, TOut, 0>(p, n_int * p.nseg, stream);
-    if (e == hipSuccess && n_all > n_int) {
-        if (quad_ok) e = launch_fused_variant<R, TY, NT, TIn, TOut, 1>(p, n_all * p.nseg, stream);
-        else e = launch_fused_variant<R, TY, NT, TIn, TOut, 2>(p, n_all * p.nseg, stream);
-    }
+    if (e == hipSuccess && n_all > n_int)
+        e = launch_fused_variant<R, TY, NT, TIn, TOut, 2>(p, n_all * p.nseg, stream);
     return e;
 }
 

@@ -32,7 +32,7 @@ struct GFParams {
     int itx0, itx1, ity0, ity1;  // interior tile range (fused kernel, host-computed)
     float eps;
     float rcp_w3;  // RN(1 / (2r+1)^3): the interior window count's reciprocal (host-computed)
-    unsigned long long* trace;  // tools/ only: s_memtime stamps of one workgroup (ABL & 16384)
+    unsigned long long* trace;  // tools/trace_steps only (tools/gf_fused_variants.hpp): per-step clock stamps of one workgroup; unused by the product kernels
     int trace_block;
 };
 
