@@ -9,7 +9,11 @@
 #include <cstdlib>
 #include <vector>
 
+#ifdef TK_V4
+#include "gf_v4.hpp"  // schedule experiment (tools/gf_v4.hpp)
+#else
 #include "../zarrs_tools_amd/csrc/gf_fused.hpp"
+#endif
 
 using namespace zt;
 #ifndef TK_TY
@@ -33,19 +37,23 @@ using namespace zt;
 int main(int argc, char** argv) {
     int n = argc > 1 ? atoi(argv[1]) : 2048;
     const char* tag = argc > 2 ? argv[2] : "";
-    size_t vox = (size_t)n * n * n;
+    // argv[4]: extra elements per row (pitch n + pad): separates the cache-set behaviour of
+    // power-of-two row pitches from the kernel's own cost
+    const int pad = argc > 4 ? atoi(argv[4]) : 0;
+    const int pitch = n + pad;
+    size_t vox = (size_t)n * n * pitch;
     float *in, *out;
     CK(hipMalloc(&in, vox * 4)); CK(hipMalloc(&out, vox * 4));
-    std::vector<float> h((size_t)n * n);
+    std::vector<float> h((size_t)n * pitch);
     for (int z = 0; z < n; ++z) {
         for (size_t i = 0; i < h.size(); ++i)
             h[i] = (float)(((i + (size_t)z * 7919u) * 2654435761u) % 1000) * 0.1f +
-                   ((i % n) < (size_t)n / 2 ? 0.0f : 500.0f);
-        CK(hipMemcpy(in + (size_t)z * n * n, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+                   ((i % pitch) < (size_t)n / 2 ? 0.0f : 500.0f);
+        CK(hipMemcpy(in + (size_t)z * n * pitch, h.data(), h.size() * 4, hipMemcpyHostToDevice));
     }
     GFParams p{};
-    p.in = in; p.out = out; p.in_sz = (int64_t)n * n; p.in_sy = n; p.out_sz = (int64_t)n * n;
-    p.out_sy = n; p.in_z0 = 0; p.zlo = 0; p.zhi = n; p.nz = p.ny = p.nx = n;
+    p.in = in; p.out = out; p.in_sz = (int64_t)n * pitch; p.in_sy = pitch; p.out_sz = (int64_t)n * pitch;
+    p.out_sy = pitch; p.in_z0 = 0; p.zlo = 0; p.zhi = n; p.nz = p.ny = p.nx = n;
     p.oz0 = p.oy0 = p.ox0 = 0; p.onz = p.ony = p.onx = n; p.zseg = (argc > 3 && atoi(argv[3]) > 0) ? atoi(argv[3]) : 256; p.eps = 2500.0f;
     hipStream_t s; CK(hipStreamCreate(&s));
     auto launch = [&](const GFParams& p0, hipStream_t st) -> hipError_t {
@@ -81,8 +89,9 @@ int main(int argc, char** argv) {
     // checksum over a few slices
     double sum = 0.0, mx = 0.0;
     for (int z : {0, 3, n / 2, n - 1}) {
-        CK(hipMemcpy(h.data(), out + (size_t)z * n * n, h.size() * 4, hipMemcpyDeviceToHost));
-        for (float v : h) { sum += v; mx = std::max(mx, (double)v); }
+        CK(hipMemcpy(h.data(), out + (size_t)z * n * pitch, h.size() * 4, hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < h.size(); ++i)
+            if ((int)(i % pitch) < n) { sum += h[i]; mx = std::max(mx, (double)h[i]); }
     }
     printf("%-24s median %8.3f ms  min %8.3f ms  checksum %.9e max %.6f\n", tag, t[2], t[0], sum,
            mx);

@@ -6,7 +6,7 @@ cd "$(dirname "$0")"
 if [ "$1" = build ]; then
   shift
   while [ $# -ge 2 ]; do
-    /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fno-gpu-flush-denormals-to-zero -fno-slp-vectorize -Xclang -target-feature -Xclang -load-store-opt $2 -o tk_$1 timek.hip 2>&1 | grep -v "not a recognized feature"
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fno-gpu-flush-denormals-to-zero -fno-slp-vectorize -Xclang -target-feature -Xclang -load-store-opt -I../zarrs_tools_amd/csrc $2 -o tk_$1 timek.hip 2>&1 | grep -v "not a recognized feature"
     shift 2
   done
 else
