@@ -203,13 +203,19 @@ def main():
     one_dev = os.environ.get("ZT_BENCH_ONE_DEVICE") == "1"
     if one_dev:
         local = 0
-    if world_env > 1:
+    # ZT_BENCH_DIST=1 under a launcher: join the process group even at one rank, so a 1-GPU box
+    # runs the RCCL init / barrier / max-reduce of the N-GPU path (tests/test_bench_gpu.py)
+    use_dist = world_env > 1 or ("WORLD_SIZE" in os.environ and
+                                 os.environ.get("ZT_BENCH_DIST") == "1")
+    backend = None
+    if use_dist:
         torch.cuda.set_device(local)
+        backend = "gloo" if one_dev else "nccl"
         if one_dev:
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    world = dist.get_world_size() if world_env > 1 else 1  # ranks RCCL actually joined
+    world = dist.get_world_size() if use_dist else 1  # ranks RCCL actually joined
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -244,7 +250,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
     ev0 = torch.cuda.Event(enable_timing=True)
@@ -255,12 +261,12 @@ def main():
         step()
     ev1.record(stream)
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if use_dist:
         dist.barrier()
     t1 = time.perf_counter()
     wall = t1 - t0
     kern_ms = ev0.elapsed_time(ev1) / args.steps  # HIP events on the launch stream
-    if world > 1:
+    if use_dist:
         tt = torch.tensor([wall, kern_ms], dtype=torch.float64,
                           device="cpu" if one_dev else dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -283,6 +289,7 @@ def main():
         "unit": "GiB/s",
         "n_gpus": 1 if one_dev else world,
         "ranks": world,
+        "dist_backend": backend,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4),
@@ -322,7 +329,7 @@ def main():
     if rank == 0:
         print(json.dumps(res), flush=True)
     ctx.close()
-    if world > 1:
+    if use_dist:
         dist.barrier()
         dist.destroy_process_group()
 

@@ -44,3 +44,28 @@ def test_bench_share_proxy_of_an_eight_way_split():
     assert r["share"]["out_z"] == [768, 1024] and r["share"]["in_z"] == [760, 1032]
     assert r["parity"]["ok"]
     assert r["share"]["projected_aggregate_gibs"] == pytest.approx(r["value"] * 8, rel=1e-3)
+
+
+def test_bench_rccl_process_group_at_one_rank():
+    """The N-GPU path's RCCL calls (init_process_group("nccl", device_id=...), barrier, MAX
+    all-reduce of the timings) on a 1-GPU box: one rank under torch.distributed.run with
+    ZT_BENCH_DIST=1."""
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env["ZT_BENCH_DIST"] = "1"
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node=1", "--master-addr", "127.0.0.1",
+                        f"--master-port={port}", os.path.join(ROOT, "bench.py"), "--size", "512",
+                        "--steps", "2", "--warmup", "1", "--parity-chunks", "2",
+                        "--no-cpu-baseline"], env=env, capture_output=True, text=True,
+                       timeout=240, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    r = json.loads(lines[0])
+    assert r["dist_backend"] == "nccl" and r["ranks"] == 1
+    assert r["parity"]["ok"] and r["value"] > 0

@@ -92,6 +92,33 @@ def test_fused_zyx_quad_staging_bit_exact(din, half):
     assert np.array_equal(out, ref)
 
 
+# Wide tiles of the fused march (ZYXWide, 32 x 256 on 1024 threads: quad marches with L <= 7 over
+# blocks at least 256 wide): several x tiles with a partial last one, chunk regions starting at
+# x = 300 (quad-aligned, not tile-aligned), partial y tiles, L = 3, 5 and 7, 1/2/4-byte inputs.
+@pytest.mark.parametrize("din,half", [("float32", 1), ("float32", 2), ("float32", 3),
+                                      ("uint16", 3), ("uint8", 2)])
+def test_fused_zyx_wide_tiles_bit_exact(din, half):
+    rng = np.random.default_rng(11 + half)
+    shape, chunk = (21, 70, 600), (21, 35, 300)
+    v32 = (rng.random(shape, dtype=np.float32) * 250).astype(np.float32)
+    v = O.cast_from_f32(v32, din)
+    sigma = [1.0, 1.3, 0.9]
+    ref = O.gaussian_apply(O.cast_to_f32(v, din), chunk, sigma, [half] * 3)
+    out = gpu_gaussian(v, din, "float32", chunk, sigma, [half] * 3)
+    assert np.array_equal(out, ref)
+    # chunk by chunk (regions at x = 0 and x = 300)
+    import itertools
+    import torch
+    x = to_dev(v, din)
+    y = torch.empty(shape, device="cuda")
+    a_in, a_out = zt.DeviceArray(x, chunk, din), zt.DeviceArray(y, chunk)
+    g = zt.Gaussian(sigma, [half] * 3)
+    for idx in itertools.product(*[range(n) for n in a_out.chunk_grid_shape()]):
+        g.apply_chunk(a_in, a_out, idx)
+    torch.cuda.synchronize()
+    assert np.array_equal(from_dev(y, "float32"), ref)
+
+
 # The fused z/y/x march (gaussian.hip gauss_zyx_kernel): one tap length L on the last three
 # axes, L in 3..13; several tiles, z segments and chunk-region offsets.
 @pytest.mark.parametrize("shape,chunk,sigma,half", [

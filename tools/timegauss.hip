@@ -35,6 +35,12 @@ namespace zt {
 #ifndef GV_NT
 #define GV_NT 256
 #endif
+#ifndef GV_LAUX
+#define GV_LAUX 0
+#endif
+#ifndef GV_PF2
+#define GV_PF2 0
+#endif
 #ifndef GV_WPE
 #define GV_WPE 4
 #endif
@@ -86,7 +92,7 @@ template <typename T>
 __device__ __forceinline__ void z_load4(zrsrc_t r, int off, float (&v)[4]) {
     if constexpr (sizeof(T) == 4) {
         typedef unsigned int u4 __attribute__((ext_vector_type(4)));
-        const u4 q = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+        const u4 q = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, GV_LAUX);
         // elements copied out first: clang's bit_cast of a vector element lvalue reads element 0
         const uint32_t w[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
@@ -195,6 +201,9 @@ __global__ __launch_bounds__(GV_NT) __attribute__((amdgpu_waves_per_eu(zyx_min_w
                 }
             };
             float ring[L][NPQ][4], pre[NPQ][4];
+#if GV_PF2
+            float pre2[NPQ][4];  // prefetch two slices ahead
+#endif
             // window of the first output slice: position i = input slice o0 + kz0 + i - MID in
             // slot i; position L - 1 arrives through pre
             // edge quads of a QUAD march: the edge element broadcast (no memory instructions,
@@ -218,6 +227,9 @@ __global__ __launch_bounds__(GV_NT) __attribute__((amdgpu_waves_per_eu(zyx_min_w
                 fix(ring[i]);
             }
             ld(p.o0[0] + kz0 + L - 1 - MID, pre);
+#if GV_PF2
+            ld(p.o0[0] + kz0 + L - MID, pre2);
+#endif
             char* obase = reinterpret_cast<char*>(out) + o * onz * ony * onx * 4;
             for (int64_t kb = kz0; kb < kz1; kb += L) {
                 static_for<0, L>([&](auto PH_) {
@@ -232,7 +244,15 @@ __global__ __launch_bounds__(GV_NT) __attribute__((amdgpu_waves_per_eu(zyx_min_w
                         for (int e = 0; e < 4; ++e) ring[(PH + L - 1) % L][k][e] = pre[k][e];
                     fix(ring[(PH + L - 1) % L]);
                     // next step's entering slice, unconditionally (clamped; unused past the end)
+#if GV_PF2
+#pragma unroll
+                    for (int k = 0; k < NPQ; ++k)
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) pre[k][e] = pre2[k][e];
+                    ld(p.o0[0] + kz + 2 + MID, pre2);
+#else
                     ld(p.o0[0] + kz + 1 + MID, pre);
+#endif
 #pragma unroll
                     for (int k = 0; k < NPQ; ++k) {
                         float sv[4];

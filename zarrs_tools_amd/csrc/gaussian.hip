@@ -403,17 +403,20 @@ __device__ __forceinline__ void z_load4(zrsrc_t r, int off, float (&v)[4]) {
 // 2 full rounds instead of 2.7.
 constexpr int zyx_min_waves(int L, bool quad) { return quad && L <= 7 ? 4 : 1; }
 
-template <int L, typename TIn, bool QUAD>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(zyx_min_waves(L, QUAD)))) void gauss_zyx_kernel(const TIn* __restrict__ in,
+// Tile shapes (output rows TY x columns TX, NT threads per workgroup).
+struct ZYXNarrow { static constexpr int TY = kZYXTy, TX = kZYXTx, NT = 256; };
+template <int L, typename TIn, bool QUAD, typename CFG = ZYXNarrow>
+__global__ __launch_bounds__(CFG::NT) __attribute__((amdgpu_waves_per_eu(CFG::NT == 256 ? zyx_min_waves(L, QUAD) : 4))) void gauss_zyx_kernel(const TIn* __restrict__ in,
                                                         float* __restrict__ out, GaussZYX p,
                                                         int tiles_x, int tiles_y, int zseg) {
-    constexpr int TY = kZYXTy, TX = kZYXTx, TH = TY + L - 1, TW = TX + L - 1, MID = L / 2;
+    constexpr int TY = CFG::TY, TX = CFG::TX, NT = CFG::NT;
+    constexpr int TH = TY + L - 1, TW = TX + L - 1, MID = L / 2;
     constexpr int MG = (MID + 3) / 4 * 4;      // x margin of the staged tile (whole quads)
     constexpr int TP = TX + 2 * MG, NQX = TP / 4;  // staged tile pitch (floats), quads per row
-    constexpr int NQ = TH * NQX, NPQ = (NQ + 255) / 256;  // quads, per thread
+    constexpr int NQ = TH * NQX, NPQ = (NQ + NT - 1) / NT;  // quads, per thread
     constexpr int NYI = TW * (TY / 4), NXI = TY * (TX / 4);  // y / x pass items
-    constexpr int NYP = (NYI + 255) / 256, NXP = (NXI + 255) / 256;
-    __shared__ __attribute__((aligned(16))) float tile[NPQ * 256 * 4];  // rows past TH: dummies
+    constexpr int NYP = (NYI + NT - 1) / NT, NXP = (NXI + NT - 1) / NT;
+    __shared__ __attribute__((aligned(16))) float tile[NPQ * NT * 4];  // rows past TH: dummies
     __shared__ float ybuf[TY * TW];
     const int tid = threadIdx.x;
     const int64_t nz = p.n[0], ny = p.n[1], nx = p.n[2];
@@ -443,7 +446,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(zyx_min_wav
         int bl = 0, br = 0;
 #pragma unroll
         for (int k = 0; k < NPQ; ++k) {
-            const int q = tid + 256 * k;
+            const int q = tid + NT * k;
             const int r = q / NQX, cq = q - r * NQX;
             int64_t qy = qy0 + r;
             qy = qy < 0 ? 0 : (qy > ny - 1 ? ny - 1 : qy);
@@ -528,14 +531,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(zyx_min_wav
                                 sum = sum + ring[(PH + i) % L][k][e] * p.w[0][i];
                             sv[e] = sum;
                         }
-                        *reinterpret_cast<float4*>(tile + 4 * (tid + 256 * k)) =
+                        *reinterpret_cast<float4*>(tile + 4 * (tid + NT * k)) =
                             make_float4(sv[0], sv[1], sv[2], sv[3]);
                     }
                     z_lds_barrier();
 #pragma unroll
                     for (int ip = 0; ip < NYP; ++ip) {  // y pass, 4 rows per item
-                        const int item = tid + 256 * ip;
-                        if (NYI % 256 == 0 || item < NYI) {
+                        const int item = tid + NT * ip;
+                        if (NYI % NT == 0 || item < NYI) {
                             // column c of the TW window = staged column c + MG - MID
                             const int c = item % TW, r0 = (item / TW) * 4;
                             float v[4 + L - 1];
@@ -556,9 +559,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(zyx_min_wav
                                               kz < kz1 ? oplane_bytes : 0u);
 #pragma unroll
                     for (int ip = 0; ip < NXP; ++ip) {  // x pass, 4 columns per item
-                        const int item = tid + 256 * ip;
+                        const int item = tid + NT * ip;
                         const int r = item / (TX / 4), c0 = (item % (TX / 4)) * 4;
-                        const bool live = (NXI % 256 == 0 || item < NXI) && r < hy;
+                        const bool live = (NXI % NT == 0 || item < NXI) && r < hy;
                         float v[4 + L - 1];
 #pragma unroll
                         for (int j = 0; j < 4 + L - 1; ++j)
@@ -603,16 +606,23 @@ bool gaussian_zyx_supported(const GaussZYX& p, int dtype_in) {
            (p.on[2] + kZYXTx - 1) / kZYXTx <= 0xFFFF;
 }
 
-template <int L>
-static hipError_t launch_zyx_l(const void* in, int dtype_in, float* out, const GaussZYX& p,
-                               hipStream_t s) {
-    const int tiles_x = (int)((p.on[2] + kZYXTx - 1) / kZYXTx);
-    const int tiles_y = (int)((p.on[1] + kZYXTy - 1) / kZYXTy);
+// Wide tiles for short quad marches (L <= 7): 4x the columns of the narrow tile on 1024 threads
+// (one workgroup per CU, 4 waves per SIMD), so the staged tile's x apron shrinks from 72/64 to
+// 264/256 columns: 1024^3 sigma = 1 measured 2.43 -> 2.13 ms in tools/timegauss.hip
+// (profiles/r03_gauss_variants_*.txt), identical output.
+struct ZYXWide { static constexpr int TY = 32, TX = 256, NT = 1024; };
+
+template <int L, typename CFG>
+static hipError_t launch_zyx_cfg(const void* in, int dtype_in, float* out, const GaussZYX& p,
+                                 bool quad, hipStream_t s) {
+    const int tiles_x = (int)((p.on[2] + CFG::TX - 1) / CFG::TX);
+    const int tiles_y = (int)((p.on[1] + CFG::TY - 1) / CFG::TY);
     const int64_t tiles = (int64_t)tiles_x * tiles_y;
     const int64_t outer = p.outer;
-    // z segments: about 4 workgroups per CU over the whole launch, at least kZYXSegMin slices
-    // each (a segment re-reads L - 1 slices to fill its window)
-    const int64_t want = (2048 + tiles * outer - 1) / (tiles * outer);
+    // z segments: about two rounds of full occupancy (4 waves per SIMD) over the launch, at
+    // least kZYXSegMin slices each (a segment re-reads L - 1 slices to fill its window)
+    const int64_t per_launch = 2 * 256 * (1024 / CFG::NT);
+    const int64_t want = (per_launch + tiles * outer - 1) / (tiles * outer);
     int64_t nseg = std::max<int64_t>(1, std::min<int64_t>(want, (p.on[0] + kZYXSegMin - 1) / kZYXSegMin));
     const int zseg = (int)((p.on[0] + nseg - 1) / nseg);
     nseg = (p.on[0] + zseg - 1) / zseg;
@@ -624,20 +634,35 @@ static hipError_t launch_zyx_l(const void* in, int dtype_in, float* out, const G
         // (quad instantiations for the common element types only: build time)
         if constexpr (std::is_same_v<T, float> || std::is_same_v<T, uint16_t> ||
                       std::is_same_v<T, uint8_t>) {
-            // quads need a 4-aligned x origin and extent and an aligned base
-            if (p.n[2] % 4 == 0 && p.o0[2] % 4 == 0 && p.n[2] >= 4 &&
-                (uintptr_t)in % (4 * sizeof(T)) == 0)
-                hipLaunchKernelGGL((gauss_zyx_kernel<L, T, true>), grid, dim3(256), 0, s,
+            if (quad)
+                hipLaunchKernelGGL((gauss_zyx_kernel<L, T, true, CFG>), grid, dim3(CFG::NT), 0, s,
                                    static_cast<const T*>(in), out, p, tiles_x, tiles_y, zseg);
-            else
-                hipLaunchKernelGGL((gauss_zyx_kernel<L, T, false>), grid, dim3(256), 0, s,
+            else if constexpr (std::is_same_v<CFG, ZYXNarrow>)
+                hipLaunchKernelGGL((gauss_zyx_kernel<L, T, false, CFG>), grid, dim3(CFG::NT), 0, s,
                                    static_cast<const T*>(in), out, p, tiles_x, tiles_y, zseg);
-        } else {
-            hipLaunchKernelGGL((gauss_zyx_kernel<L, T, false>), grid, dim3(256), 0, s,
+        } else if constexpr (std::is_same_v<CFG, ZYXNarrow>) {  // (wide tiles: quad marches only)
+            hipLaunchKernelGGL((gauss_zyx_kernel<L, T, false, CFG>), grid, dim3(CFG::NT), 0, s,
                                static_cast<const T*>(in), out, p, tiles_x, tiles_y, zseg);
         }
         err = hipGetLastError())
     return err;
+}
+
+template <int L>
+static hipError_t launch_zyx_l(const void* in, int dtype_in, float* out, const GaussZYX& p,
+                               hipStream_t s) {
+    const int esz = dtype_size(dtype_in);
+    // quads need a 4-aligned x origin and extent and an aligned base, <= 4-byte elements
+    const bool quad = esz <= 4 && p.n[2] % 4 == 0 && p.o0[2] % 4 == 0 &&
+                      p.n[2] >= 4 && (uintptr_t)in % (4 * esz) == 0 &&
+                      (dtype_in == kF32 || dtype_in == kU16 || dtype_in == kU8 || dtype_in == kBool);
+    // wide tiles when the march is a short quad march and the block is wide enough not to
+    // leave most of a wide tile idle
+    if constexpr (L <= 7) {
+        if (quad && p.on[2] >= ZYXWide::TX)
+            return launch_zyx_cfg<L, ZYXWide>(in, dtype_in, out, p, quad, s);
+    }
+    return launch_zyx_cfg<L, ZYXNarrow>(in, dtype_in, out, p, quad, s);
 }
 
 hipError_t launch_gaussian_zyx(const void* in, int dtype_in, float* out, const GaussZYX& p,
