@@ -176,10 +176,12 @@ def load_traffic(gshape, radius: int, world: int):
     try:
         with open(path) as f:
             d = json.load(f)
-        if (d.get("lib_sha256") == lib_hash() and list(d.get("global_shape", [])) == list(gshape)
-                and d.get("radius") == radius and d.get("world", 1) == world):
-            return d.get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
+        entries = d.get("entries", [d]) if isinstance(d, dict) else list(d)
+        for e in entries:  # one entry per measured workload (G3 r=4, G2 r=2, ...)
+            if (e.get("lib_sha256") == lib_hash() and list(e.get("global_shape", [])) == list(gshape)
+                    and e.get("radius") == radius and e.get("world", 1) == world):
+                return e.get("hbm_bytes_per_launch")
+    except (OSError, ValueError, AttributeError):
         pass
     return None
 

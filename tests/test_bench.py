@@ -48,3 +48,24 @@ def test_gpus_must_match_world_size(monkeypatch):
     assert e.value.code == 2
     A.gpus = 2
     bench.maybe_launch(A())  # under a launcher with the matching count: no-op
+
+
+def test_traffic_entries_are_keyed_to_build_workload_and_world(monkeypatch, tmp_path):
+    import json
+    (tmp_path / "profiles").mkdir()
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    monkeypatch.setattr(bench, "lib_hash", lambda: "abc")
+    entries = [{"lib_sha256": "abc", "global_shape": [2048] * 3, "radius": 4, "world": 1,
+                "hbm_bytes_per_launch": 1.0e11},
+               {"lib_sha256": "abc", "global_shape": [1024] * 3, "radius": 2, "world": 1,
+                "hbm_bytes_per_launch": 2.0e10},
+               {"lib_sha256": "old", "global_shape": [512] * 3, "radius": 2, "world": 1,
+                "hbm_bytes_per_launch": 3.0e9}]
+    (tmp_path / "profiles" / "pmc_traffic.json").write_text(json.dumps({"entries": entries}))
+    assert bench.load_traffic((2048,) * 3, 4, 1) == 1.0e11
+    assert bench.load_traffic((1024,) * 3, 2, 1) == 2.0e10
+    assert bench.load_traffic((512,) * 3, 2, 1) is None  # measured on another build
+    assert bench.load_traffic((2048,) * 3, 4, 2) is None  # another world size
+    # the single-entry form of earlier rounds still reads
+    (tmp_path / "profiles" / "pmc_traffic.json").write_text(json.dumps(entries[0]))
+    assert bench.load_traffic((2048,) * 3, 4, 1) == 1.0e11

@@ -3,7 +3,7 @@
 the FETCH_SIZE / WRITE_SIZE passes of tools/profile_pmc.sh, keyed to the library build (sha256),
 the workload and the world size, so bench.py only reports it for the build it was measured on.
 
-Usage: make_traffic_json.py PMC_DIR OUT_JSON [size radius]
+Usage: make_traffic_json.py PMC_DIR OUT_JSON [size radius]  (merges into OUT_JSON's entries)
 Method (MI355X_MICROARCH.md, HBM / rocprofv3): one launch (bench.py --steps 1 --warmup 0), each
 counter in its own run; FETCH_SIZE and WRITE_SIZE are KiB; FETCH_SIZE x2 is the gfx950
 correction for wide (128 B) reads counted as 64 B.
@@ -49,8 +49,20 @@ def main():
          "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate runs of bench.py "
                    "--steps 1 --warmup 0; FETCH_SIZE x2 (gfx950 wide-read correction), KiB -> "
                    "bytes; Infinity-Cache hits are counted by these counters"}
+    # merge: one entry per (shape, radius, world); entries of other builds are dropped
+    entries = []
+    if os.path.exists(out):
+        try:
+            old = json.load(open(out))
+            entries = old.get("entries", [old]) if isinstance(old, dict) else list(old)
+        except ValueError:
+            entries = []
+    entries = [e for e in entries if e.get("lib_sha256") == d["lib_sha256"] and
+               (e.get("global_shape"), e.get("radius"), e.get("world", 1)) !=
+               (d["global_shape"], d["radius"], d["world"])]
+    entries.append(d)
     with open(out, "w") as f:
-        json.dump(d, f, indent=1)
+        json.dump({"entries": entries}, f, indent=1)
     print(json.dumps(d))
 
 
