@@ -19,6 +19,12 @@
 
 // Tuning knobs (tools/timek.hip sweeps them with -D; profiles/r02_ab_harness.txt). Variants that
 // were measured slower live only in tools/gf_fused_variants.hpp.
+#ifndef GF4_PF2
+#define GF4_PF2 0  // stage-1 slices prefetched two steps ahead (a second register set)
+#endif
+#ifndef GF4_UNI
+#define GF4_UNI 0  // mode 1: block-uniform count path for tiles whose E2 apron is inside the domain
+#endif
 #ifndef GF4_WPE
 #define GF4_WPE 4
 #endif
@@ -583,6 +589,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(GF4_WPE))) v
 
     const int x0 = p.ox0 + tile_x * TX;
     const int y0 = p.oy0 + tile_y * TY;
+    // the tile's whole E2 apron inside the domain in x and y (block-uniform)
+    const bool xyfull = x0 - 2 * R >= 0 && x0 + TX + 2 * R <= p.nx && y0 - 2 * R >= 0 &&
+                        y0 + TY + 2 * R <= p.ny;
     const int ox_end = p.ox0 + p.onx, oy_end = p.oy0 + p.ony;
     const int zo_begin = p.oz0 + seg * p.zseg;
     const int zo_end = min(zo_begin + p.zseg, p.oz0 + p.onz);
@@ -666,11 +675,14 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(GF4_WPE))) v
 
     // ---- phase bodies ----------------------------------------------------------------------
     float pa[C::NQP1][EPL], ps[C::NQP1][EPL];  // P1 inputs of the next stage-1 slice (prefetched)
+#if GF4_PF2
+    float pa2[C::NQP1][EPL], ps2[C::NQP1][EPL];  // ... and of the one after (in flight)
+#endif
     float vc[C::K3];  // v of the next P3 slice at this thread's item (prefetched)
     float v5[K5];     // v of the next P5 output slice at this thread's outputs
 #pragma unroll
     for (int j = 0; j < K5; ++j) v5[j] = 0.0f;
-    auto load_p1 = [&](rsrc_t ra, rsrc_t rs) {  // entering slice zc+R, leaving slice zc-R-1
+    auto load_p1_into = [&](rsrc_t ra, rsrc_t rs, float (&da)[C::NQP1][EPL], float (&ds)[C::NQP1][EPL]) {
 #pragma unroll
         for (int k = 0; k < C::NQP1; ++k) {
             float a4[4], s4[4];
@@ -678,10 +690,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(GF4_WPE))) v
             load_quad(rs, q1off[k], q1mask[k], s4);
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                pa[k][e] = a4[e];
-                ps[k][e] = s4[e];
+                da[k][e] = a4[e];
+                ds[k][e] = s4[e];
             }
         }
+    };
+    auto load_p1 = [&](rsrc_t ra, rsrc_t rs) {  // entering slice zc+R, leaving slice zc-R-1
+        load_p1_into(ra, rs, pa, ps);
     };
     // P12: z-window of v (f64, running) and its x-window sums on the E2 apron -> Hx. The x
     // neighbours come from the adjacent lanes' quads by DPP wave shifts (whole rows per wave),
@@ -786,7 +801,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(GF4_WPE))) v
             Uf[k] = (f2){(float)U[2 * k], (float)U[2 * k + 1]};
             vv[k] = (f2){vc[2 * k], vc[2 * k + 1]};  // v of slice zc, loaded a half-step ago
         }
-        if constexpr (INTERIOR) {
+        if (INTERIOR || (GF4_UNI && xyfull)) {
             // every E1 point of the tile has the full x and y windows: count = W^2 * cz(zc)
             // (wave-uniform); planes outside the domain hold no (a, b)
             const bool zin = (unsigned)zc < (unsigned)nz;
@@ -894,7 +909,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(GF4_WPE))) v
         // is clamped so its table index stays valid there
         const int zq = min(max(zo, 0), nz - 1);
         f2 rc[K5];
-        if constexpr (INTERIOR) {
+        if (INTERIOR || (GF4_UNI && xyfull)) {
             const float r = rcp_tab[W * W * clamped_count(zq, nz, R)];  // wave-uniform
 #pragma unroll
             for (int j = 0; j < K5; ++j) rc[j] = (f2){r, r};
@@ -955,6 +970,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(GF4_WPE))) v
     load_p3v(slice_rsrc(zc_begin));
     do_p12(tid0, hx_of(zc_begin));
     load_p1(slice_rsrc(zc_begin + 1 + R), slice_rsrc(zc_begin - R));
+#if GF4_PF2
+    load_p1_into(slice_rsrc(zc_begin + 2 + R), slice_rsrc(zc_begin + 1 - R), pa2, ps2);
+#endif
     lds_barrier();
 
     // ---- slice streams: descriptors advanced by one slice per step (two 32-bit adds each)
@@ -1027,7 +1045,19 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(GF4_WPE))) v
             load_p5v(rs_in(ob - sstride, zb - 1));                // P5 slice i-R
             if constexpr (C::ORDER & 2) do_p4(tid, i);
             do_p12(tid, hx_of(i + 1));
+#if GF4_PF2
+#pragma unroll
+            for (int kk = 0; kk < C::NQP1; ++kk)
+#pragma unroll
+                for (int e = 0; e < EPL; ++e) {
+                    pa[kk][e] = pa2[kk][e];
+                    ps[kk][e] = ps2[kk][e];
+                }
+            load_p1_into(rs_in(ob + off_a + sstride, zb + 2 * R + 2), rs_in(ob + sstride, zb + 1),
+                         pa2, ps2);
+#else
             load_p1(rs_in(ob + off_a, zb + 2 * R + 1), r_b);
+#endif
             if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(1);
             if constexpr (!(C::ORDER & 2)) do_p4(tid, i);
             lds_barrier();
