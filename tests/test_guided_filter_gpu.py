@@ -122,6 +122,25 @@ def test_all_input_types(din):
     assert rel_err(out, ref) <= FLOAT_TOL
 
 
+# 8- and 16-bit integer inputs take the fused kernel's integer stage 1 (exact int32 window sums,
+# 4-byte Hx rows): full-range values (W^3 * 65535 near 2^31 at r = 8), eps down to 0.5 (where a
+# 1-ulp error in u shows), quad-aligned geometry (one mode-1 grid) and odd widths (masked edge
+# tiles), whole array and chunk by chunk.
+@pytest.mark.parametrize("din", ["uint16", "uint8"])
+@pytest.mark.parametrize("r", [1, 2, 3, 4, 5, 8])
+def test_integer_inputs_stage1_exact(din, r):
+    rng = np.random.default_rng(100 + r)
+    top = 65535 if din == "uint16" else 255
+    for shape, chunk in [((12, 40, 136), (6, 16, 64)), ((11, 37, 91), (5, 13, 30))]:
+        v = rng.integers(0, top + 1, size=shape).astype(din)
+        for eps in (0.5, 2500.0):
+            ref = O.guided_filter_apply(O.cast_to_f32(v, din), chunk, eps, r, nthreads=8)
+            out = gpu_apply(v, din, "float32", chunk, eps, r)
+            assert rel_err(out, ref) <= FLOAT_TOL, (shape, eps)
+        out = gpu_apply_chunked(v, din, "float32", chunk, eps, r)
+        assert rel_err(out, ref) <= FLOAT_TOL, (shape, "per chunk")
+
+
 @pytest.mark.parametrize("dout", list(O.DTYPES))
 def test_all_output_types(dout):
     v = O.synth_step_noise_f32((6, 13, 70)) * np.float32(0.4)

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -26,6 +27,12 @@ using namespace zt;
 #define TK_NT 1024
 #endif
 
+#ifdef TK_U16
+using TIN = uint16_t;  // integer input (-DTK_U16): the stage-1 integer path
+#else
+using TIN = float;
+#endif
+
 #ifndef TK_LAUNCH
 #define TK_LAUNCH 0  // 0: launch_fused_cfg; 1: mode 1 over every tile; 2: mode 0 over every tile
                      // (timing only: the border tiles' output is wrong)
@@ -42,14 +49,19 @@ int main(int argc, char** argv) {
     const int pad = argc > 4 ? atoi(argv[4]) : 0;
     const int pitch = n + pad;
     size_t vox = (size_t)n * n * pitch;
-    float *in, *out;
-    CK(hipMalloc(&in, vox * 4)); CK(hipMalloc(&out, vox * 4));
+    TIN* in;
+    float* out;
+    CK(hipMalloc(&in, vox * sizeof(TIN))); CK(hipMalloc(&out, vox * 4));
     std::vector<float> h((size_t)n * pitch);
+    std::vector<TIN> hi((size_t)n * pitch);
     for (int z = 0; z < n; ++z) {
-        for (size_t i = 0; i < h.size(); ++i)
+        for (size_t i = 0; i < h.size(); ++i) {
             h[i] = (float)(((i + (size_t)z * 7919u) * 2654435761u) % 1000) * 0.1f +
                    ((i % pitch) < (size_t)n / 2 ? 0.0f : 500.0f);
-        CK(hipMemcpy(in + (size_t)z * n * pitch, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+            hi[i] = std::is_same<TIN, float>::value ? (TIN)h[i] : (TIN)(h[i] * 10.0f);
+        }
+        CK(hipMemcpy(in + (size_t)z * n * pitch, hi.data(), hi.size() * sizeof(TIN),
+                     hipMemcpyHostToDevice));
     }
     GFParams p{};
     p.in = in; p.out = out; p.in_sz = (int64_t)n * pitch; p.in_sy = pitch; p.out_sz = (int64_t)n * pitch;
@@ -57,7 +69,7 @@ int main(int argc, char** argv) {
     p.oz0 = p.oy0 = p.ox0 = 0; p.onz = p.ony = p.onx = n; p.zseg = (argc > 3 && atoi(argv[3]) > 0) ? atoi(argv[3]) : 256; p.eps = 2500.0f;
     hipStream_t s; CK(hipStreamCreate(&s));
     auto launch = [&](const GFParams& p0, hipStream_t st) -> hipError_t {
-        if (TK_LAUNCH == 0) return launch_fused_cfg<TK_R, TK_TY, TK_NT, float, float>(p0, st);
+        if (TK_LAUNCH == 0) return launch_fused_cfg<TK_R, TK_TY, TK_NT, TIN, float>(p0, st);
         using C = GFConfig<TK_R, TK_TY, TK_NT>;
         GFParams q = p0;
         volatile float one = 1.0f;
@@ -68,10 +80,10 @@ int main(int argc, char** argv) {
         const long long nwg = (long long)q.tiles_x * q.tiles_y * q.nseg;
         if (TK_LAUNCH == 1) {
             q.itx0 = q.itx1 = q.ity0 = q.ity1 = 0;
-            return launch_fused_variant<TK_R, TK_TY, TK_NT, float, float, 1>(q, nwg, st);
+            return launch_fused_variant<TK_R, TK_TY, TK_NT, TIN, float, 1>(q, nwg, st);
         }
         q.itx0 = 0; q.itx1 = q.tiles_x; q.ity0 = 0; q.ity1 = q.tiles_y;
-        return launch_fused_variant<TK_R, TK_TY, TK_NT, float, float, 0>(q, nwg, st);
+        return launch_fused_variant<TK_R, TK_TY, TK_NT, TIN, float, 0>(q, nwg, st);
     };
     hipEvent_t a, b;
     CK(hipEventCreate(&a)); CK(hipEventCreate(&b));

@@ -253,12 +253,12 @@ struct RingDispatch<W, W> {
 // matters: a = s/(s+eps) with s = (v-u)^2 is ill-conditioned in u for small eps, so u must be
 // the reference's u bit for bit.
 // ---------------------------------------------------------------------------------------------
-template <int R, int K>
-__device__ __forceinline__ void slide_sums_f64(const double (&in)[K + 2 * R], double (&out)[K]) {
-    // exact sums: any association gives the same value, so the first window is a balanced
-    // tree and each later one adds an independently formed difference (chain depth
-    // log2(W) + K - 1 instead of 2R + 2(K - 1))
-    double c[2 * R + 1];
+template <int R, int K, typename T>
+__device__ __forceinline__ void slide_sums_exact(const T (&in)[K + 2 * R], T (&out)[K]) {
+    // exact sums (f64 of f32 values, or 32-bit integers): any association gives the same
+    // value, so the first window is a balanced tree and each later one adds an independently
+    // formed difference (chain depth log2(W) + K - 1 instead of 2R + 2(K - 1))
+    T c[2 * R + 1];
 #pragma unroll
     for (int j = 0; j <= 2 * R; ++j) c[j] = in[j];
 #pragma unroll
@@ -266,13 +266,25 @@ __device__ __forceinline__ void slide_sums_f64(const double (&in)[K + 2 * R], do
 #pragma unroll
         for (int j = 0; j + w <= 2 * R; j += 2 * w) c[j] = c[j] + c[j + w];
     }
-    double d[K];
+    T d[K];
 #pragma unroll
     for (int i = 1; i < K; ++i) d[i] = in[i + 2 * R] - in[i - 1];
     out[0] = c[0];
 #pragma unroll
     for (int i = 1; i < K; ++i) out[i] = out[i - 1] + d[i];
 }
+
+// Stage-1 arithmetic per input type. 8- and 16-bit integer inputs are summed exactly in 32-bit
+// integers (a window of W^3 <= 17^3 values of at most 65535 stays below 2^31): the same U as the
+// reference's f64 SAT of their `as f32` values, at one 2-cycle add per term instead of f64
+// conversions and adds, one DPP move per neighbour instead of two, and 4-byte Hx elements.
+template <typename T> struct S1 {
+    using acc = double;  // window sums
+    using in = float;    // loaded stage-1 values
+    static constexpr int HXB = 8;
+};
+template <> struct S1<uint8_t> { using acc = int; using in = int; static constexpr int HXB = 4; };
+template <> struct S1<uint16_t> { using acc = int; using in = int; static constexpr int HXB = 4; };
 
 // s / (s + eps): rcp + one Newton step + Markstein correction (6 VALU ops instead of the ~12 of
 // IEEE division; within 1 ulp, almost always correctly rounded). Special values follow IEEE:
@@ -334,6 +346,9 @@ template <> struct Buf<uint16_t> {
     __device__ static float load(rsrc_t r, int off) {
         return (float)(uint16_t)__builtin_amdgcn_raw_buffer_load_b16(r, off, 0, AUX);
     }
+    __device__ static int load_int(rsrc_t r, int off) {
+        return (int)(uint16_t)__builtin_amdgcn_raw_buffer_load_b16(r, off, 0, 0);
+    }
     __device__ static void store(uint16_t v, rsrc_t r, int off) {
         __builtin_amdgcn_raw_buffer_store_b16(v, r, off, 0, 2);
     }
@@ -342,6 +357,9 @@ template <> struct Buf<uint8_t> {
     template <int AUX = 0>
     __device__ static float load(rsrc_t r, int off) {
         return (float)(uint8_t)__builtin_amdgcn_raw_buffer_load_b8(r, off, 0, AUX);
+    }
+    __device__ static int load_int(rsrc_t r, int off) {
+        return (int)(uint8_t)__builtin_amdgcn_raw_buffer_load_b8(r, off, 0, 0);
     }
     __device__ static void store(uint8_t v, rsrc_t r, int off) {
         __builtin_amdgcn_raw_buffer_store_b8(v, r, off, 0, 2);
@@ -360,6 +378,12 @@ __device__ __forceinline__ double dpp_from_upper(double v) {
     const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0x130, 0xF, 0xF, true);
     const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0x130, 0xF, 0xF, true);
     return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ int dpp_from_lower(int v) {
+    return __builtin_amdgcn_mov_dpp(v, 0x138, 0xF, 0xF, true);
+}
+__device__ __forceinline__ int dpp_from_upper(int v) {
+    return __builtin_amdgcn_mov_dpp(v, 0x130, 0xF, 0xF, true);
 }
 
 // ---- 4 consecutive elements (one 16/8/4-byte buffer access per lane) ----------------------
@@ -389,6 +413,11 @@ template <> struct Quad<uint16_t> {
         v[0] = (float)(q.x & 0xffffu); v[1] = (float)(q.x >> 16);
         v[2] = (float)(q.y & 0xffffu); v[3] = (float)(q.y >> 16);
     }
+    __device__ static void load(rsrc_t r, int off, int (&v)[4]) {
+        const u32x2 q = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+        v[0] = (int)(q.x & 0xffffu); v[1] = (int)(q.x >> 16);
+        v[2] = (int)(q.y & 0xffffu); v[3] = (int)(q.y >> 16);
+    }
     __device__ static void store(const float (&v)[4], rsrc_t r, int off) {
         const uint32_t a = (uint32_t)from_f32<uint16_t>(v[0]) | ((uint32_t)from_f32<uint16_t>(v[1]) << 16);
         const uint32_t b = (uint32_t)from_f32<uint16_t>(v[2]) | ((uint32_t)from_f32<uint16_t>(v[3]) << 16);
@@ -401,6 +430,11 @@ template <> struct Quad<uint8_t> {
         const uint32_t q = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, AUX);
         v[0] = (float)(q & 0xffu); v[1] = (float)((q >> 8) & 0xffu);
         v[2] = (float)((q >> 16) & 0xffu); v[3] = (float)(q >> 24);
+    }
+    __device__ static void load(rsrc_t r, int off, int (&v)[4]) {
+        const uint32_t q = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
+        v[0] = (int)(q & 0xffu); v[1] = (int)((q >> 8) & 0xffu);
+        v[2] = (int)((q >> 16) & 0xffu); v[3] = (int)(q >> 24);
     }
     __device__ static void store(const float (&v)[4], rsrc_t r, int off) {
         const uint32_t a = (uint32_t)from_f32<uint8_t>(v[0]) | ((uint32_t)from_f32<uint8_t>(v[1]) << 8) |
@@ -426,6 +460,12 @@ __device__ __forceinline__ void load_quad_masked(rsrc_t r, int off, int mask, fl
         v[e] = Buf<T>::load(r, (mask >> e) & 1 ? off + e * (int)sizeof(T) : kBadOff);
 }
 template <typename T>
+__device__ __forceinline__ void load_quad_masked(rsrc_t r, int off, int mask, int (&v)[4]) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+        v[e] = Buf<T>::load_int(r, (mask >> e) & 1 ? off + e * (int)sizeof(T) : kBadOff);
+}
+template <typename T>
 __device__ __forceinline__ void store_quad_masked(const float (&v)[4], rsrc_t r, int off, int mask) {
 #pragma unroll
     for (int e = 0; e < 4; ++e)
@@ -445,16 +485,20 @@ __device__ __forceinline__ void store_quad_masked(const float (&v)[4], rsrc_t r,
 // interior tiles: the kernel is bound by vector-memory instruction issue otherwise (one dword
 // per lane cost about as much as the whole pointwise stage).
 // ---------------------------------------------------------------------------------------------
-template <int R, int TY, int NT>
+template <int R, int TY, int NT, int HXB = 8>
 struct GFConfig {
     static constexpr int TX = 64;
     static constexpr int W = 2 * R + 1;
+    static constexpr int HXB_ = HXB;  // bytes per Hx element
     static constexpr int E2X = TX + 4 * R, E2Y = TY + 4 * R;  // v / Zv apron
     static constexpr int E1X = TX + 2 * R, E1Y = TY + 2 * R;  // u / a / b apron
     // Pitches in 8-byte elements, = 2 mod 4: 16-B aligned rows and conflict-free ds_*_b128
     // when lanes walk rows (16-lane groups land on distinct 4-bank slots).
     static constexpr int p2m4(int x) { return x + ((2 - x % 4) + 4) % 4; }
-    static constexpr int PH = p2m4(E1X);  // Hx  (f64)    P12 writes rows, P3 reads columns
+    // Hx (f64, or int32 for 8/16-bit integer inputs; HXB bytes): P12 writes rows, P3 reads
+    // columns. 4-byte rows: pitch a multiple of 4 (16-byte aligned rows) and not of 8.
+    static constexpr int ph4(int x) { return (x + 3) / 4 * 4 + ((x + 3) / 4 * 4 % 8 == 0 ? 4 : 0); }
+    static constexpr int PH = HXB == 8 ? p2m4(E1X) : ph4(E1X);
     static constexpr int PA = p2m4(E1X);  // Lab (float2) P3 writes, P4 reads rows
     static constexpr int PB = p2m4(TX);   // Hab (float2) P4 writes rows, P5 reads columns
     // r = 4 (the headline radius, 64 x 32 tiles): 8 outputs per P4 item and P4 issued ahead of
@@ -480,7 +524,7 @@ struct GFConfig {
     static constexpr int NQ5 = TX / 4 * TY;                  // output tile quads
     static constexpr int W3 = W * W * W;                     // interior window count
     static constexpr int al(int b) { return (b + 255) / 256 * 256; }
-    static constexpr int SZ_HX = al((E2Y + K3) * PH * 8);
+    static constexpr int SZ_HX = al((E2Y + K3) * PH * HXB);
     static constexpr int SZ_LAB = al((E1Y + 1) * PA * 8);
     static constexpr int SZ_HAB = al((E1Y + 1) * PB * 8);
     static constexpr int SZ_RCP = al((W3 + 1) * 4);  // RN(1/c) for window counts c <= W^3
@@ -514,13 +558,15 @@ struct GFConfig {
 // every load).
 template <int R, int TY, int NT, typename TIn, typename TOut, int MODE>
 __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
-    using C = GFConfig<R, TY, NT>;
+    using C = GFConfig<R, TY, NT, S1<TIn>::HXB>;
+    using SA = typename S1<TIn>::acc;  // stage-1 window sums (exact)
+    using SI = typename S1<TIn>::in;   // loaded stage-1 values
     constexpr bool EDGE = MODE == 2, INTERIOR = MODE == 0;
     constexpr int TX = C::TX, W = C::W;
     constexpr int K5 = C::K5;
     constexpr int ESZ = (int)sizeof(TIn), OSZ = (int)sizeof(TOut);
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    double* const Hx = reinterpret_cast<double*>(smem + C::OFF_HX);
+    SA* const Hx = reinterpret_cast<SA*>(smem + C::OFF_HX);
     float2* const Lab = reinterpret_cast<float2*>(smem + C::OFF_LAB);
     float2* const Hab = reinterpret_cast<float2*>(smem + C::OFF_HAB);
     float* const rcp_tab = reinterpret_cast<float*>(smem + C::OFF_RCP);
@@ -616,16 +662,16 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
         q1mask[k] = m;
         q1off[k] = (EDGE ? valid : m == 0xF) ? (gy * sy + gx) * ESZ : kBadOff;
     }
-    auto load_quad = [&](rsrc_t r, int off, int mask, float (&v)[4]) {
+    auto load_quad = [&](rsrc_t r, int off, int mask, SI (&v)[4]) {
         if constexpr (EDGE) load_quad_masked<TIn>(r, off, mask, v);
         else Quad<TIn>::load(r, off, v);
     };
 
-    double zv[C::NQP1][EPL];
+    SA zv[C::NQP1][EPL];
 #pragma unroll
     for (int k = 0; k < C::NQP1; ++k)
 #pragma unroll
-        for (int e = 0; e < EPL; ++e) zv[k][e] = 0.0;
+        for (int e = 0; e < EPL; ++e) zv[k][e] = (SA)0;
     // Running z-window: seed Zv(zc_begin - 1) = sum of v over [zc_begin-1-R, zc_begin-1+R]
     // clamped to [0, nz); every later step adds the entering and subtracts the leaving slice
     // (both 0 outside the domain), so the window stays exact through out-of-domain steps.
@@ -635,10 +681,10 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
             const rsrc_t rs = slice_rsrc(z);
 #pragma unroll
             for (int k = 0; k < C::NQP1; ++k) {
-                float v[4];
+                SI v[4];
                 load_quad(rs, q1off[k], q1mask[k], v);
 #pragma unroll
-                for (int e = 0; e < 4; ++e) zv[k][e] += (double)v[e];
+                for (int e = 0; e < 4; ++e) zv[k][e] += (SA)v[e];
             }
         }
     }
@@ -652,7 +698,7 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     for (int j = 0; j < K5; ++j) pre[j] = (f2){0.0f, 0.0f};
 
     // ---- phase bodies ----------------------------------------------------------------------
-    float pa[C::NQP1][EPL], ps[C::NQP1][EPL];  // P1 inputs of the next stage-1 slice (prefetched)
+    SI pa[C::NQP1][EPL], ps[C::NQP1][EPL];  // P1 inputs of the next stage-1 slice (prefetched)
     float vc[C::K3];  // v of the next P3 slice at this thread's item (prefetched)
     float v5[K5];     // v of the next P5 output slice at this thread's outputs
 #pragma unroll
@@ -660,7 +706,7 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     auto load_p1 = [&](rsrc_t ra, rsrc_t rs) {  // entering slice zc+R, leaving slice zc-R-1
 #pragma unroll
         for (int k = 0; k < C::NQP1; ++k) {
-            float a4[4], s4[4];
+            SI a4[4], s4[4];
             load_quad(ra, q1off[k], q1mask[k], a4);
             load_quad(rs, q1off[k], q1mask[k], s4);
 #pragma unroll
@@ -680,11 +726,11 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
             const bool valid = p12_pos(tid, k, row, cq);
 #pragma unroll
             for (int e = 0; e < EPL; ++e) {
-                zv[k][e] = zv[k][e] + (double)pa[k][e];  // entering slice (0 outside the domain)
-                zv[k][e] = zv[k][e] - (double)ps[k][e];  // leaving slice (0 outside the domain)
+                zv[k][e] = zv[k][e] + (SA)pa[k][e];  // entering slice (0 outside the domain)
+                zv[k][e] = zv[k][e] - (SA)ps[k][e];  // leaving slice (0 outside the domain)
             }
             constexpr int NB = C::NB;
-            double win[EPL * (2 * NB + 1)];  // lane items cq-NB .. cq+NB
+            SA win[EPL * (2 * NB + 1)];  // lane items cq-NB .. cq+NB
 #pragma unroll
             for (int e = 0; e < EPL; ++e) win[EPL * NB + e] = zv[k][e];
             // only the R elements next to the own item are read (the others' moves are dead)
@@ -695,11 +741,25 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
                     win[EPL * (NB - n) + e] = dpp_from_lower(win[EPL * (NB - n + 1) + e]);
                     win[EPL * (NB + n) + e] = dpp_from_upper(win[EPL * (NB + n - 1) + e]);
                 }
-            double vin[EPL + 2 * R], hs[EPL];
+            SA vin[EPL + 2 * R], hs[EPL];
 #pragma unroll
             for (int j = 0; j < EPL + 2 * R; ++j) vin[j] = win[EPL * NB - R + j];
-            slide_sums_f64<R, EPL>(vin, hs);
-            if constexpr (GF_HX_B128 && R % 2 == 0) {
+            slide_sums_exact<R, EPL>(vin, hs);
+            if constexpr (C::HXB_ == 4 && R % 4 == 0) {
+                // int32 rows: the item's 4 outputs are one 16-byte aligned quad of Hx
+                const int col4 = EPL * cq - R;
+                if (valid && col4 >= 0 && col4 + 3 < C::E1X)
+                    *reinterpret_cast<int4*>(Hx + row * C::PH + col4) =
+                        make_int4(hs[0], hs[1], hs[2], hs[3]);
+            } else if constexpr (C::HXB_ == 4 && R % 2 == 0) {
+#pragma unroll
+                for (int h = 0; h < EPL / 2; ++h) {
+                    const int colh = EPL * cq + 2 * h - R;
+                    if (valid && colh >= 0 && colh + 1 < C::E1X)
+                        *reinterpret_cast<int2*>(Hx + row * C::PH + colh) =
+                            make_int2(hs[2 * h], hs[2 * h + 1]);
+                }
+            } else if constexpr (C::HXB_ == 8 && GF_HX_B128 && R % 2 == 0) {
                 // even R: the item's outputs land on 16-byte aligned column pairs of Hx (E1X and
                 // the pitch are even): b128 writes (b64 writes of lanes 32 B apart conflict)
 #pragma unroll
@@ -760,11 +820,11 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
         const int item = tid - C::T3;
         if (item < 0) return;
         const int col = item % C::E1X, sg = item / C::E1X;
-        const double* src = Hx + (sg * C::K3) * C::PH + col;
-        double vin[C::K3 + 2 * R], U[C::K3];
+        const SA* src = Hx + (sg * C::K3) * C::PH + col;
+        SA vin[C::K3 + 2 * R], U[C::K3];
 #pragma unroll
         for (int j = 0; j < C::K3 + 2 * R; ++j) vin[j] = src[j * C::PH];
-        slide_sums_f64<R, C::K3>(vin, U);
+        slide_sums_exact<R, C::K3>(vin, U);
         f2* lab = reinterpret_cast<f2*>(Lab);
         f2 Uf[NP3], vv[NP3], fc[NP3], rc[NP3], a[NP3], bb[NP3];
 #pragma unroll
@@ -1043,7 +1103,7 @@ inline hipError_t allow_dynamic_lds(const void* kern, int bytes, std::atomic<uin
 
 template <int R, int TY, int NT, typename TIn, typename TOut, int MODE>
 inline hipError_t launch_fused_variant(const GFParams& p, long long nwg, hipStream_t stream) {
-    using C = GFConfig<R, TY, NT>;
+    using C = GFConfig<R, TY, NT, S1<TIn>::HXB>;
     const size_t lds = (size_t)C::LDS_BYTES;
     auto kern = gf3d_fused_kernel<R, TY, NT, TIn, TOut, MODE>;
     if (hipError_t e = allow_dynamic_lds((const void*)kern, (int)lds, attr_devices<decltype(kern)>()))
