@@ -3,7 +3,7 @@
 # bench line, its kernel-trace stats, the PMC passes of the fused kernel (SQ, FETCH, WRITE, TCC)
 # and the traffic entry keyed to this build. Each step under its own limit; any failure ends it.
 set -u
-OUT=gpurun_out/r3fa
+OUT=gpurun_out/${1:-r3fa}
 ROOT=$(pwd)
 mkdir -p $OUT
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -rf --timeout 600 --timeout-method thread > $OUT/pytest.log 2>&1; rc=$?

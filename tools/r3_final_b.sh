@@ -4,7 +4,7 @@
 # (T share, pyramid, Gaussian) with kernel-trace stats; config P's 4096^3 pyramid.
 # Usage: tools/r3_final_b.sh [traffic json to merge into]
 set -u
-OUT=gpurun_out/r3fb
+OUT=gpurun_out/${2:-r3fb}
 ROOT=$(pwd)
 mkdir -p $OUT
 timeout -k 10 300 python3 -u bench.py --size 1024 --radius 2 --steps 20 --warmup 3 > $OUT/bench_g2.json 2> $OUT/bench_g2.err || { tail $OUT/bench_g2.err; exit 1; }
