@@ -82,6 +82,26 @@ int main(int argc, char** argv) {
             q.itx0 = q.itx1 = q.ity0 = q.ity1 = 0;
             return launch_fused_variant<TK_R, TK_TY, TK_NT, TIN, float, 1>(q, nwg, st);
         }
+        if (TK_LAUNCH == 3) {
+            // interior tiles in mode 0 on `st`, the border tiles in mode 1 concurrently on a
+            // second stream (launched first), joined back into `st`
+            static hipStream_t s2 = nullptr;
+            static hipEvent_t e0, e1;
+            if (!s2) {
+                CK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+                CK(hipEventCreateWithFlags(&e0, hipEventDisableTiming));
+                CK(hipEventCreateWithFlags(&e1, hipEventDisableTiming));
+            }
+            interior_tiles(q.ox0, q.ox0 + q.onx, q.nx, C::TX, TK_R, 0, q.tiles_x, q.itx0, q.itx1);
+            interior_tiles(q.oy0, q.oy0 + q.ony, q.ny, TK_TY, TK_R, 0, q.tiles_y, q.ity0, q.ity1);
+            const long long n_int = (long long)(q.itx1 - q.itx0) * (q.ity1 - q.ity0) * q.nseg;
+            CK(hipEventRecord(e0, st));
+            CK(hipStreamWaitEvent(s2, e0, 0));
+            CK((launch_fused_variant<TK_R, TK_TY, TK_NT, TIN, float, 1>(q, nwg, s2)));
+            CK(hipEventRecord(e1, s2));
+            CK((launch_fused_variant<TK_R, TK_TY, TK_NT, TIN, float, 0>(q, n_int, st)));
+            return hipStreamWaitEvent(st, e1, 0);
+        }
         q.itx0 = 0; q.itx1 = q.tiles_x; q.ity0 = 0; q.ity1 = q.tiles_y;
         return launch_fused_variant<TK_R, TK_TY, TK_NT, TIN, float, 0>(q, nwg, st);
     };
