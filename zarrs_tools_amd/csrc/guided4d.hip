@@ -53,6 +53,12 @@ __device__ __forceinline__ int ccount(int i, int n, int r) {
 }
 
 constexpr int kTX = 64, kTY = 16, kNT = 256, kKX = 4, kKY = 4;
+constexpr int kPX = 64, kPY = 4;  // K2 / K4 thread blocks: 4 rows of 64 x
+// element strides of a (T, nz, ny, nx) input with unit-stride x (the chunk's halo'd box read in
+// place from the resident array, or a C-order scratch copy)
+struct Str3 {
+    int64_t t, z, y;
+};
 
 // 3-D window sums (radius R, clamped to the volume) of every timepoint volume of a (T, nz, ny, nx)
 // C-order array: a workgroup marches one 64 x 16 xy tile through zseg slices of one timepoint.
@@ -62,7 +68,7 @@ template <int R, typename TV, typename TA, typename TO>
 __global__ __launch_bounds__(kNT) void box3_march_kernel(const TV* __restrict__ in,
                                                          TO* __restrict__ out, int nz, int ny,
                                                          int nx, int zseg, int tiles_x,
-                                                         int tiles_y) {
+                                                         int tiles_y, Str3 is) {
     constexpr int EX = kTX + 2 * R, EY = kTY + 2 * R, NE = EX * EY;
     constexpr int NPT = (NE + kNT - 1) / kNT;
     __shared__ TA Z[EY][EX];
@@ -73,7 +79,7 @@ __global__ __launch_bounds__(kNT) void box3_march_kernel(const TV* __restrict__ 
     const int x0 = (tile % tiles_x) * kTX, y0 = (tile / tiles_x) * kTY;
     const int z0 = seg * zseg, z1 = min(z0 + zseg, nz);
     const int64_t plane = (int64_t)ny * nx;
-    const TV* vol = in + (int64_t)t * nz * plane;
+    const TV* vol = in + (int64_t)t * is.t;  // input: strided (x unit-stride); output: C order
     TO* ovol = out + (int64_t)t * nz * plane;
 
     // owned apron points: index into the plane (or -1 outside the volume / past the apron)
@@ -86,10 +92,10 @@ __global__ __launch_bounds__(kNT) void box3_march_kernel(const TV* __restrict__ 
         const int gy = y0 - R + ey, gx = x0 - R + ex;
         ey_[k] = e < NE ? ey : -1;
         ex_[k] = ex;
-        pidx[k] = (e < NE && gy >= 0 && gy < ny && gx >= 0 && gx < nx) ? (int64_t)gy * nx + gx : -1;
+        pidx[k] = (e < NE && gy >= 0 && gy < ny && gx >= 0 && gx < nx) ? (int64_t)gy * is.y + gx : -1;
     }
     auto load = [&](int z, int k) -> TV {
-        return (pidx[k] >= 0 && z >= 0 && z < nz) ? vol[(int64_t)z * plane + pidx[k]] : zero_v<TV>();
+        return (pidx[k] >= 0 && z >= 0 && z < nz) ? vol[(int64_t)z * is.z + pidx[k]] : zero_v<TV>();
     };
     TA zs[NPT];
 #pragma unroll
@@ -156,17 +162,18 @@ __global__ __launch_bounds__(kNT) void box3_march_kernel(const TV* __restrict__ 
 }
 
 // K2: u, s, a, b for every timepoint of a voxel (guided_filter.rs:126-142) with 4-D counts.
-// One thread per x of a (z, y) row (3-D grid: no 64-bit index division); the T values of U3
-// are read once into registers (T <= TMAX at compile time).
+// One thread per (y, x) of a 4 x 64 block (3-D grid: no 64-bit index division; 64-wide rows keep
+// a chunk's 264-wide halo'd rows 83 % busy where 256-wide rows left half the lanes idle); the T
+// values of U3 are read once into registers (T <= TMAX at compile time).
 template <int TMAX>
 __global__ __launch_bounds__(256) void g4_pointwise_kernel(const double* __restrict__ U3,
                                                            const float* __restrict__ v,
                                                            float2* __restrict__ AB, int T,
                                                            int ta_ab, int tb_ab, int nz, int ny,
-                                                           int nx, int r, float eps) {
+                                                           int nx, int r, float eps, Str3 vs) {
     const int64_t vol = (int64_t)nz * ny * nx;
-    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
-    if (x >= nx) return;
+    const int x = blockIdx.x * kPX + threadIdx.x, y = blockIdx.y * kPY + threadIdx.y;
+    if (x >= nx || y >= ny) return;
     const int cyx = ccount(y, ny, r) * ccount(x, nx, r);
     for (int z = blockIdx.z; z < nz; z += gridDim.z) {
         const int64_t i = ((int64_t)z * ny + y) * nx + x;
@@ -184,7 +191,7 @@ __global__ __launch_bounds__(256) void g4_pointwise_kernel(const double* __restr
                 if (tt >= ta && tt <= tb) U4 += U[tt];
             const float cnt = (float)(c3 * (tb - ta + 1));
             const float u = (float)U4 / cnt;  // summed_area_table_mean: (sum as f32) / count
-            const float d = v[t * vol + i] - u;
+            const float d = v[t * vs.t + (int64_t)z * vs.z + (int64_t)y * vs.y + x] - u;
             const float s = d * d;  // (v - u).powf(2.0)
             const float a = s / (s + eps);
             const float b = (1.0f - a) * u;
@@ -197,23 +204,28 @@ __global__ __launch_bounds__(256) void g4_pointwise_kernel(const double* __restr
 template <int TMAX, typename TOut>
 __global__ __launch_bounds__(256) void g4_final_kernel(const float2* __restrict__ S3,
                                                        const float* __restrict__ v,
-                                                       TOut* __restrict__ out, NdGeom g, int r) {
+                                                       TOut* __restrict__ out, NdGeom g, int r,
+                                                       Str3 vs) {
     const int T = (int)g.shape[0], nz = (int)g.shape[1], ny = (int)g.shape[2],
               nx = (int)g.shape[3];
     const int64_t vol = (int64_t)nz * ny * nx;
-    const int ox = blockIdx.x * 256 + threadIdx.x, oy = blockIdx.y;
-    if (ox >= (int)g.out_shape[3]) return;
+    const int ox = blockIdx.x * kPX + threadIdx.x, oy = blockIdx.y * kPY + threadIdx.y;
+    if (ox >= (int)g.out_shape[3] || oy >= (int)g.out_shape[2]) return;
     const int x = ox + (int)g.out_start[3], y = oy + (int)g.out_start[2];
     const int cyx = ccount(y, ny, r) * ccount(x, nx, r);
     const int t0 = (int)g.out_start[0], ont = (int)g.out_shape[0];
+    const int tlo = max(t0 - r, 0), thi = min(t0 + ont + r, T);
     for (int oz = blockIdx.z; oz < (int)g.out_shape[1]; oz += gridDim.z) {
         const int z = oz + (int)g.out_start[1];
         const int64_t bi = ((int64_t)z * ny + y) * nx + x;
         const int c3 = ccount(z, nz, r) * cyx;
         const int64_t dbase = oz * g.out_strides[1] + oy * g.out_strides[2] + ox * g.out_strides[3];
+        // only the timepoints the output windows read (a slab's outer halo timepoints feed
+        // stage 1 alone)
         float2 S[TMAX];
 #pragma unroll
-        for (int t = 0; t < TMAX; ++t) S[t] = t < T ? S3[t * vol + bi] : make_float2(0.f, 0.f);
+        for (int t = 0; t < TMAX; ++t)
+            S[t] = t >= tlo && t < thi ? S3[t * vol + bi] : make_float2(0.f, 0.f);
 #pragma unroll
         for (int ot = 0; ot < TMAX; ++ot) {
             if (ot >= ont) continue;
@@ -228,14 +240,16 @@ __global__ __launch_bounds__(256) void g4_final_kernel(const float2* __restrict_
                 }
             const float cnt = (float)(c3 * (tb - ta + 1));
             const float ma = (float)sa / cnt, mb = (float)sb / cnt;
-            const float o = __fadd_rn(__fmul_rn(v[t * vol + bi], ma), mb);  // v *= ma; v += mb
+            const float vv = v[t * vs.t + (int64_t)z * vs.z + (int64_t)y * vs.y + x];
+            const float o = __fadd_rn(__fmul_rn(vv, ma), mb);  // v *= ma; v += mb
             out[dbase + ot * g.out_strides[0]] = from_f32<TOut>(o);
         }
     }
 }
 
 template <int R, typename TV, typename TA, typename TO>
-hipError_t launch_box3(const TV* in, TO* out, int T, int nz, int ny, int nx, hipStream_t s) {
+hipError_t launch_box3(const TV* in, TO* out, int T, int nz, int ny, int nx, Str3 is,
+                       hipStream_t s) {
     const int tiles_x = (nx + kTX - 1) / kTX, tiles_y = (ny + kTY - 1) / kTY;
     const int64_t tiles = (int64_t)tiles_x * tiles_y;
     // z segments: enough workgroups for the chip (>= ~4 per CU), at least 16 slices each
@@ -245,20 +259,20 @@ hipError_t launch_box3(const TV* in, TO* out, int T, int nz, int ny, int nx, hip
     const int64_t gx = tiles * nseg;
     if (gx > 0x7FFFFFFF || T > 65535) return hipErrorInvalidValue;
     hipLaunchKernelGGL((box3_march_kernel<R, TV, TA, TO>), dim3((unsigned)gx, (unsigned)T),
-                       dim3(kNT), 0, s, in, out, nz, ny, nx, zseg, tiles_x, tiles_y);
+                       dim3(kNT), 0, s, in, out, nz, ny, nx, zseg, tiles_x, tiles_y, is);
     return hipGetLastError();
 }
 
 template <typename TV, typename TA, typename TO>
-hipError_t launch_box3_r(int r, const TV* in, TO* out, int T, int nz, int ny, int nx,
+hipError_t launch_box3_r(int r, const TV* in, TO* out, int T, int nz, int ny, int nx, Str3 is,
                          hipStream_t s) {
     switch (r) {
-    case 1: return launch_box3<1, TV, TA, TO>(in, out, T, nz, ny, nx, s);
-    case 2: return launch_box3<2, TV, TA, TO>(in, out, T, nz, ny, nx, s);
-    case 3: return launch_box3<3, TV, TA, TO>(in, out, T, nz, ny, nx, s);
-    case 4: return launch_box3<4, TV, TA, TO>(in, out, T, nz, ny, nx, s);
-    case 5: return launch_box3<5, TV, TA, TO>(in, out, T, nz, ny, nx, s);
-    case 6: return launch_box3<6, TV, TA, TO>(in, out, T, nz, ny, nx, s);
+    case 1: return launch_box3<1, TV, TA, TO>(in, out, T, nz, ny, nx, is, s);
+    case 2: return launch_box3<2, TV, TA, TO>(in, out, T, nz, ny, nx, is, s);
+    case 3: return launch_box3<3, TV, TA, TO>(in, out, T, nz, ny, nx, is, s);
+    case 4: return launch_box3<4, TV, TA, TO>(in, out, T, nz, ny, nx, is, s);
+    case 5: return launch_box3<5, TV, TA, TO>(in, out, T, nz, ny, nx, is, s);
+    case 6: return launch_box3<6, TV, TA, TO>(in, out, T, nz, ny, nx, is, s);
     default: return hipErrorInvalidValue;
     }
 }
@@ -283,17 +297,13 @@ hipError_t launch_guided4d(const void* in, int dtype_in, void* out, int dtype_ou
     char* base = static_cast<char*>(scratch);
     double* U3 = reinterpret_cast<double*>(base);          // later S3 (float2) in place
     float2* AB = reinterpret_cast<float2*>(base + n * 8);
-    bool contiguous = dtype_in == kF32;
-    {
-        int64_t st = 1;
-        for (int d = 3; d >= 0; --d) {
-            if (g.in_strides[d] != st) contiguous = false;
-            st *= g.shape[d];
-        }
-    }
+    // f32 with unit-stride x is read in place (strided t / z / y); other element types or
+    // strides are first copied to C-order f32 in scratch
+    const bool in_place = dtype_in == kF32 && g.in_strides[3] == 1;
     const float* v = static_cast<const float*>(in);
+    Str3 vs{g.in_strides[0], g.in_strides[1], g.in_strides[2]};
     hipError_t e;
-    if (!contiguous) {
+    if (!in_place) {
         float* vv = reinterpret_cast<float*>(base + n * 16);
         for (int t = 0; t < T; ++t) {
             const size_t esz = dtype_size(dtype_in);
@@ -303,22 +313,25 @@ hipError_t launch_guided4d(const void* in, int dtype_in, void* out, int dtype_ou
             if (e != hipSuccess) return e;
         }
         v = vv;
+        vs = Str3{(int64_t)nz * ny * nx, (int64_t)ny * nx, (int64_t)nx};
     }
-    e = launch_box3_r<float, double, double>(radius, v, U3, T, nz, ny, nx, s);
+    e = launch_box3_r<float, double, double>(radius, v, U3, T, nz, ny, nx, vs, s);
     if (e != hipSuccess) return e;
     if (ny > 65535 || g.out_shape[2] > 65535) return hipErrorInvalidValue;  // grid.y
     // (a, b) are needed only within R timepoints of the output's (a slab's halo timepoints
     // beyond that feed stage 1 alone)
     const int ta_ab = std::max<int>(0, (int)g.out_start[0] - radius);
     const int tb_ab = std::min<int>(T, (int)(g.out_start[0] + g.out_shape[0]) + radius);
-    const dim3 pgrid((unsigned)((nx + 255) / 256), (unsigned)ny,
-                     (unsigned)std::min<int64_t>(nz, std::max<int64_t>(1, 65536 / ((int64_t)ny * ((nx + 255) / 256)) + 1)));
+    const int64_t pgx = (nx + kPX - 1) / kPX, pgy = (ny + kPY - 1) / kPY;
+    const dim3 pgrid((unsigned)pgx, (unsigned)pgy,
+                     (unsigned)std::min<int64_t>(nz, std::max<int64_t>(1, 65536 / (pgy * pgx) + 1)));
+    const dim3 pblock(kPX, kPY);
     if (T <= 4)
-        hipLaunchKernelGGL(g4_pointwise_kernel<4>, pgrid, dim3(256), 0, s, U3, v, AB, T, ta_ab,
-                           tb_ab, nz, ny, nx, radius, eps);
+        hipLaunchKernelGGL(g4_pointwise_kernel<4>, pgrid, pblock, 0, s, U3, v, AB, T, ta_ab,
+                           tb_ab, nz, ny, nx, radius, eps, vs);
     else if (T <= 16)
-        hipLaunchKernelGGL(g4_pointwise_kernel<16>, pgrid, dim3(256), 0, s, U3, v, AB, T, ta_ab,
-                           tb_ab, nz, ny, nx, radius, eps);
+        hipLaunchKernelGGL(g4_pointwise_kernel<16>, pgrid, pblock, 0, s, U3, v, AB, T, ta_ab,
+                           tb_ab, nz, ny, nx, radius, eps, vs);
     else
         return hipErrorInvalidValue;
     if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -326,22 +339,24 @@ hipError_t launch_guided4d(const void* in, int dtype_in, void* out, int dtype_ou
     {  // K3 on the timepoints whose (a, b) sums K4 reads
         const int64_t vol = (int64_t)nz * ny * nx;
         e = launch_box3_r<float2, dd2, float2>(radius, AB + ta_ab * vol, S3 + ta_ab * vol,
-                                               tb_ab - ta_ab, nz, ny, nx, s);
+                                               tb_ab - ta_ab, nz, ny, nx,
+                                               Str3{vol, (int64_t)ny * nx, (int64_t)nx}, s);
     }
     if (e != hipSuccess) return e;
     const int64_t onx = g.out_shape[3], ony = g.out_shape[2], onz = g.out_shape[1];
-    const dim3 fgrid((unsigned)((onx + 255) / 256), (unsigned)ony,
-                     (unsigned)std::min<int64_t>(onz, std::max<int64_t>(1, 65536 / (ony * ((onx + 255) / 256)) + 1)));
+    const int64_t fgx = (onx + kPX - 1) / kPX, fgy = (ony + kPY - 1) / kPY;
+    const dim3 fgrid((unsigned)fgx, (unsigned)fgy,
+                     (unsigned)std::min<int64_t>(onz, std::max<int64_t>(1, 65536 / (fgy * fgx) + 1)));
     e = hipErrorInvalidValue;
     if (T <= 4) {
         ZT_DISPATCH_DTYPE(dtype_out, TO,
-            hipLaunchKernelGGL((g4_final_kernel<4, TO>), fgrid, dim3(256), 0, s, S3, v,
-                               static_cast<TO*>(out), g, radius);
+            hipLaunchKernelGGL((g4_final_kernel<4, TO>), fgrid, dim3(kPX, kPY), 0, s, S3, v,
+                               static_cast<TO*>(out), g, radius, vs);
             e = hipGetLastError())
     } else {
         ZT_DISPATCH_DTYPE(dtype_out, TO,
-            hipLaunchKernelGGL((g4_final_kernel<16, TO>), fgrid, dim3(256), 0, s, S3, v,
-                               static_cast<TO*>(out), g, radius);
+            hipLaunchKernelGGL((g4_final_kernel<16, TO>), fgrid, dim3(kPX, kPY), 0, s, S3, v,
+                               static_cast<TO*>(out), g, radius, vs);
             e = hipGetLastError())
     }
     return e;
