@@ -355,3 +355,41 @@ def test_guided4d_fused_chunk_grid_subset():
     mask = np.ones(v.shape, bool)
     mask[box] = False
     assert np.all(out[mask] == -1)
+
+
+# Launch grouping of the separable / four-kernel 4-D paths: with a scratch budget too small for
+# the whole box (ZT_SCRATCH_LIMIT), chunks are grouped into rows over the trailing axes (or run
+# one by one); every grouping equals the oracle. Each budget runs in its own process (the
+# library reads the variable per call, torch state stays out of the parent).
+@pytest.mark.parametrize("case", ["4d_rows", "4d_chunks", "3d_rows"])
+def test_chunk_row_grouping_under_a_scratch_budget(case):
+    import subprocess
+    import sys
+    code = f"""
+import numpy as np, torch, sys
+sys.path.insert(0, {os.path.dirname(os.path.dirname(os.path.abspath(__file__)))!r})
+from oracle import oracle as O
+from tests.test_guided_filter_gpu import gpu_apply
+from tests.gpu_util import rel_err, FLOAT_TOL
+case = {case!r}
+rng = np.random.default_rng(5)
+if case.startswith("4d"):
+    shape, chunk, r = (6, 40, 30, 70), (2, 8, 8, 32), 2
+else:
+    shape, chunk, r = (60, 40, 70), (8, 8, 32), 9
+v = (rng.random(shape, dtype=np.float32) * 300).astype(np.float32)
+ref = O.guided_filter_apply(v, chunk, 0.5, r, nthreads=8)
+out = gpu_apply(v, "float32", "float32", chunk, 0.5, r)
+e = rel_err(out, ref)
+assert e <= FLOAT_TOL, e
+print("ok", e)
+"""
+    # budgets: 4d_rows fits one (t, z) row of chunks (+ halo) but not the whole box; 4d_chunks
+    # fits one chunk only; 3d_rows fits one z row of the separable path
+    # (four-kernel scratch 20 B per input voxel, separable 5 f32 words; whole boxes 10.1 / 3.4 MB)
+    limit = {"4d_rows": 20 * 6 * 16 * 30 * 70 + 64, "4d_chunks": 20 * 6 * 16 * 16 * 40 + 64,
+             "3d_rows": 20 * 44 * 40 * 70 + 64}[case]
+    env = dict(os.environ, ZT_SCRATCH_LIMIT=str(limit))
+    p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                       timeout=240)
+    assert p.returncode == 0 and "ok" in p.stdout, p.stderr[-2000:]

@@ -629,44 +629,50 @@ int zt_guided_filter_apply_array(zt_ctx* ctx, int dtype_in, const void* in, int 
     }
     int64_t ov[ZT_MAX_DIMS];
     for (int d = 0; d < ndim; ++d) ov[d] = (int64_t)((radius * 2) & 0xFF);
-    // Separable path, whole box at once when its scratch (5 f32 words per voxel of the box plus
-    // its 2r halo) fits in half the free device memory: chunked == whole with the halo
-    // (SURVEY.md §0.2), and a contiguous f32 array is then read in place.
-    {
-        int64_t is0[ZT_MAX_DIMS], ish[ZT_MAX_DIMS], dst[ZT_MAX_DIMS];
-        int rc = zt_subset_overlap(shape, ndim, ostart, oshape, ov, is0, ish, dst);
-        if (rc) return rc;
-        size_t free_b = 0, total_b = 0;
-        const bool g4 = use_guided4d(ndim, radius, strides, ish);
-        const size_t need =
-            g4 ? (size_t)zt::guided4d_scratch_bytes(numel(ish, ndim), true)
-               : sizeof(float) * (size_t)zt::separable_scratch_floats(numel(ish, ndim));
-        const bool have = ctx->scratch_bytes >= need ||
-                          (hipMemGetInfo(&free_b, &total_b) == hipSuccess &&
-                           need + ctx->scratch_bytes <= free_b / 2);
-        (void)hipGetLastError();
-        if (have) {
-            int64_t ioff = 0, ooff = 0;
-            for (int d = 0; d < ndim; ++d) {
-                ioff += is0[d] * strides[d];
-                ooff += ostart[d] * strides[d];
-            }
-            if (g4)
-                return run_guided4d(ctx, dtype_in, static_cast<const char*>(in) + esz_in * ioff,
-                                    ish, strides, dst, oshape, dtype_out,
-                                    static_cast<char*>(out) + esz_out * ooff, strides, epsilon,
-                                    radius);
-            return run_separable(ctx, dtype_in, static_cast<const char*>(in) + esz_in * ioff,
-                                 ish, strides, ndim, dst, oshape, dtype_out,
-                                 static_cast<char*>(out) + esz_out * ooff, strides, epsilon,
-                                 radius);
-        }
+    // Separable / four-kernel 4-D paths: as few launches as the scratch allows. Chunks are
+    // grouped along the trailing axes — the whole box when its scratch (plus its 2r halo) fits
+    // in half the free device memory, else rows of chunks over axes k..ndim-1 for the smallest k
+    // that fits, down to single chunks. Chunked == whole with the halo; rows
+    // spare the per-chunk halo recompute of the grouped axes and the launches' tails.
+    size_t free_b = 0, total_b = 0;
+    const bool have_info = hipMemGetInfo(&free_b, &total_b) == hipSuccess;
+    (void)hipGetLastError();
+    auto need_of = [&](const int64_t* ish) -> size_t {
+        return use_guided4d(ndim, radius, strides, ish)
+                   ? (size_t)zt::guided4d_scratch_bytes(numel(ish, ndim), true)
+                   : sizeof(float) * (size_t)zt::separable_scratch_floats(numel(ish, ndim));
+    };
+    // ZT_SCRATCH_LIMIT (bytes, tests): a smaller budget, to exercise the row / chunk grouping
+    const char* lim_env = getenv("ZT_SCRATCH_LIMIT");
+    const size_t lim = lim_env ? (size_t)strtoull(lim_env, nullptr, 10) : SIZE_MAX;
+    auto fits = [&](size_t need) {
+        if (need > lim) return false;
+        return ctx->scratch_bytes >= need ||
+               (have_info && need + ctx->scratch_bytes <= free_b / 2);
+    };
+    // k = number of leading axes iterated chunk by chunk (0: the whole box in one call). A
+    // group's input is at most one chunk plus its two halos along axes < k and the box (plus
+    // its halos) along the rest; the budget check uses that largest group.
+    int64_t bis0[ZT_MAX_DIMS], bish[ZT_MAX_DIMS], bdst[ZT_MAX_DIMS];
+    if (int rc = zt_subset_overlap(shape, ndim, ostart, oshape, ov, bis0, bish, bdst)) return rc;
+    int k = 0;
+    for (; k < ndim; ++k) {
+        int64_t ish[ZT_MAX_DIMS];
+        for (int d = 0; d < ndim; ++d)
+            ish[d] = d < k ? std::min(chunk_shape[d] + 2 * ov[d], bish[d]) : bish[d];
+        if (fits(need_of(ish))) break;
     }
-    // Otherwise chunk by chunk, each reading its 2r halo from the resident array.
-    int64_t nchunks = numel(gn, ndim);
-    for (int64_t c = 0; c < nchunks; ++c) {
+    // iterate the chunk grid of axes < k; each call covers those chunks' full extent along >= k
+    int64_t ngroups = 1;
+    for (int d = 0; d < k; ++d) ngroups *= gn[d];
+    for (int64_t c = 0; c < ngroups; ++c) {
         int64_t rem = c, cs[ZT_MAX_DIMS], csh[ZT_MAX_DIMS];
         for (int d = ndim - 1; d >= 0; --d) {
+            if (d >= k) {
+                cs[d] = ostart[d];
+                csh[d] = oshape[d];
+                continue;
+            }
             int64_t ci = g0[d] + rem % gn[d];
             rem /= gn[d];
             cs[d] = ci * chunk_shape[d];
