@@ -76,7 +76,9 @@ def main():
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     e0.record(stream)
+    levels = None
     for _ in range(a.steps):
+        levels = None  # free the previous step's levels first (caching allocator reuse)
         levels = step()
     e1.record(stream)
     torch.cuda.synchronize()
