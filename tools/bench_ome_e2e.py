@@ -22,6 +22,9 @@ def main():
     ap.add_argument("--levels", type=int, default=5)
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--dir", default=os.environ.get("TMPDIR", "/tmp"))
+    ap.add_argument("--gpus", type=int, nargs="*", default=[],
+                    help="also run zarrs_ome --gpus N for each N, every process on device 0 "
+                         "(a one-GPU rehearsal of the octant split)")
     a = ap.parse_args()
     import numpy as np
     from oracle import oracle as O
@@ -38,27 +41,31 @@ def main():
                          "cache)", "config": {"shape": shape, "chunk": [a.chunk] * 3,
                                                "dtype": "uint16", "levels": a.levels,
                                                "host_threads": a.threads}}
-        for mode, dev in (("device_resident", True), ("store_loop", False)):
+        modes = [("device_resident", True, 1), ("store_loop", False, 1)]
+        modes += [(f"octants_{g}_procs_one_gpu", True, g) for g in a.gpus]
+        # parity reference: a corner block of every level by the oracle chain (never timed)
+        blk = min(64, a.size)
+        refs, ref = [], S.read_array(pin, (0, 0, 0), (blk,) * 3)
+        for lvl in range(1, a.levels + 1):
+            ref = O.downsample(ref, "uint16", (2, 2, 2), "uint16")
+            refs.append(ref)
+            if min(ref.shape) <= 1:
+                break
+        ok = True
+        for mode, dev, g in modes:
             out = os.path.join(work, mode)
             t0 = time.perf_counter()
+            kw = {"gpus": g, "gpu_devices": [0] * g} if g > 1 else {}
             r = ZO.run(pin, out, max_levels=a.levels, nthreads=a.threads, log=lambda *x: None,
-                       device_resident=dev)
+                       device_resident=dev, **kw)
             wall = time.perf_counter() - t0
             res[mode] = {"wall_s": round(wall, 3), "levels": r["levels"],
                          "input_gvox_per_s": round(a.size ** 3 / wall / 1e9, 3),
                          "level_s": [round(st["wall_s"], 3) for st in r["stats"]]}
-        # parity: a corner block of every level vs the oracle chain on the same block
-        blk = min(64, a.size)
-        ref = S.read_array(pin, (0, 0, 0), (blk,) * 3)
-        ok = True
-        for lvl in range(1, res["device_resident"]["levels"] + 1):
-            ref = O.downsample(ref, "uint16", (2, 2, 2), "uint16")
-            n = ref.shape
-            for mode in ("device_resident", "store_loop"):
-                got = S.read_array(os.path.join(work, mode, str(lvl)), (0, 0, 0), n)
-                ok = ok and bool(np.array_equal(got, ref))
-            if min(n) <= 1:
-                break
+            for lvl, want in enumerate(refs[:r["levels"]], start=1):
+                got = S.read_array(os.path.join(out, str(lvl)), (0, 0, 0), want.shape)
+                ok = ok and bool(np.array_equal(got, want))
+            shutil.rmtree(out, ignore_errors=True)  # (disk: one output at a time)
         res["parity"] = {"bit_exact_corner_blocks": ok}
         print(json.dumps(res), flush=True)
     finally:

@@ -52,7 +52,14 @@ __device__ __forceinline__ int ccount(int i, int n, int r) {
     return hi - lo + 1;
 }
 
-constexpr int kTX = 64, kTY = 16, kNT = 256, kKX = 4, kKY = 4;
+#ifndef G4_BOX_TY
+#define G4_BOX_TY 16  // box3 march tile height (tools/timeg4rows.hip A/B)
+#endif
+#ifndef G4_BOX_KY
+#define G4_BOX_KY 4  // y-window outputs per thread; kTX * kTY / kKY must equal kNT
+#endif
+constexpr int kTX = 64, kTY = G4_BOX_TY, kNT = 256, kKX = 4, kKY = G4_BOX_KY;
+static_assert(kTX * (kTY / kKY) == kNT, "the y-window items cover the tile once");
 constexpr int kPX = 64, kPY = 4;  // K2 / K4 thread blocks: 4 rows of 64 x
 // element strides of a (T, nz, ny, nx) input with unit-stride x (the chunk's halo'd box read in
 // place from the resident array, or a C-order scratch copy)
