@@ -35,6 +35,9 @@ namespace zt {
 #ifndef GV_NT
 #define GV_NT 256
 #endif
+#ifndef GV_XQ
+#define GV_XQ 0
+#endif
 #ifndef GV_LAUX
 #define GV_LAUX 0
 #endif
@@ -136,7 +139,14 @@ __global__ __launch_bounds__(GV_NT) __attribute__((amdgpu_waves_per_eu(zyx_min_w
     constexpr int NYI = TW * (TY / 4), NXI = TY * (TX / 4);  // y / x pass items
     constexpr int NYP = (NYI + GV_NT - 1) / GV_NT, NXP = (NXI + GV_NT - 1) / GV_NT;
     __shared__ __attribute__((aligned(16))) float tile[NPQ * GV_NT * 4];  // rows past TH: dummies
-    __shared__ float ybuf[TY * TW];
+#if GV_XQ
+    // x-pass rows read as 16-byte quads: pitch a multiple of 4 floats (lanes 16 B apart are
+    // conflict-free for ds_read_b128; single floats 16 B apart were 4-way bank conflicts)
+    constexpr int YP = (TW + 3) / 4 * 4 + 4 * ((((TW + 3) / 4) % 2) == 0 ? 1 : 0);
+#else
+    constexpr int YP = TW;
+#endif
+    __shared__ __attribute__((aligned(16))) float ybuf[TY * YP];
     const int tid = threadIdx.x;
     const int64_t nz = p.n[0], ny = p.n[1], nx = p.n[2];
     const int64_t onz = p.on[0], ony = p.on[1], onx = p.on[2];
@@ -283,7 +293,7 @@ __global__ __launch_bounds__(GV_NT) __attribute__((amdgpu_waves_per_eu(zyx_min_w
                                 float sum = -0.0f;
 #pragma unroll
                                 for (int i = 0; i < L; ++i) sum = sum + v[k + i] * p.w[1][i];
-                                ybuf[(r0 + k) * TW + c] = sum;
+                                ybuf[(r0 + k) * YP + c] = sum;
                             }
                         }
                     }
@@ -296,9 +306,26 @@ __global__ __launch_bounds__(GV_NT) __attribute__((amdgpu_waves_per_eu(zyx_min_w
                         const int r = item / (TX / 4), c0 = (item % (TX / 4)) * 4;
                         const bool live = (NXI % GV_NT == 0 || item < NXI) && r < hy;
                         float v[4 + L - 1];
+#if GV_XQ
+                        {
+                            constexpr int NV = 4 + L - 1, NQ4 = NV / 4;
+                            const float* rowp = ybuf + (live ? r : 0) * YP + c0;
+#pragma unroll
+                            for (int q = 0; q < NQ4; ++q) {
+                                const float4 f = *reinterpret_cast<const float4*>(rowp + 4 * q);
+                                v[4 * q] = f.x; v[4 * q + 1] = f.y; v[4 * q + 2] = f.z; v[4 * q + 3] = f.w;
+                            }
+                            if constexpr (NV % 4 >= 2) {
+                                const float2 f = *reinterpret_cast<const float2*>(rowp + 4 * NQ4);
+                                v[4 * NQ4] = f.x; v[4 * NQ4 + 1] = f.y;
+                            }
+                            if constexpr (NV % 2 == 1) v[NV - 1] = rowp[NV - 1];
+                        }
+#else
 #pragma unroll
                         for (int j = 0; j < 4 + L - 1; ++j)
-                            v[j] = ybuf[(live ? r : 0) * TW + c0 + j];
+                            v[j] = ybuf[(live ? r : 0) * YP + c0 + j];
+#endif
                         float o4[4];
 #pragma unroll
                         for (int k = 0; k < 4; ++k) {
