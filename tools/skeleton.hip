@@ -92,25 +92,52 @@ __global__ __launch_bounds__(NT) void skeleton_kernel(const float* __restrict__ 
     const int zo_begin = seg * zseg, zo_end = min(zo_begin + zseg, n);
     const int tid = threadIdx.x;
 
-    const int o1 = apron_off<SK_M1>(tid, x0, y0, n);   // stage-1 apron quad
-    const int o3 = apron_off<R>(tid, x0, y0, n);       // P3 apron quad
-    const int o5 = apron_off<0>(tid, x0, y0, n);       // tile quad (P5 v and the output)
-    const int o1l = SK_NOLEAVE ? -1 : o1, o3l = SK_NOP3 ? -1 : o3, o5l = SK_NOP5 ? -1 : o5;
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    // seed: the z-window before the first stage-1 slice (2R + 1 slices)
-    for (int z = zo_begin - 2 * R - 1; z < zo_begin; ++z) {
-        const float4 e = ld(in, slice, n, z, o1);
-        acc.x += e.x; acc.y += e.y; acc.z += e.z; acc.w += e.w;
+    // items per thread of the stage-1 and P3 aprons (more than one for tiles wider than 64)
+    constexpr int K1 = ((TX + 2 * SK_M1) / 4 * (TY + 2 * SK_M1) + NT - 1) / NT;
+    constexpr int K3 = ((TX + 2 * R) / 4 * (TY + 2 * R) + NT - 1) / NT;
+    int o1[K1], o1l[K1], o3l[K3];
+#pragma unroll
+    for (int k = 0; k < K1; ++k) {
+        o1[k] = apron_off<SK_M1>(tid + k * NT, x0, y0, n);  // stage-1 apron quad
+        o1l[k] = SK_NOLEAVE ? -1 : o1[k];
     }
+#pragma unroll
+    for (int k = 0; k < K3; ++k) o3l[k] = SK_NOP3 ? -1 : apron_off<R>(tid + k * NT, x0, y0, n);
+    const int o5 = apron_off<0>(tid, x0, y0, n);  // tile quad (P5 v and the output)
+    const int o5l = SK_NOP5 ? -1 : o5;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    auto add = [&](const float4& e, float sgn) {
+        acc.x += sgn * e.x; acc.y += sgn * e.y; acc.z += sgn * e.z; acc.w += sgn * e.w;
+    };
+    // seed: the z-window before the first stage-1 slice (2R + 1 slices)
+    for (int z = zo_begin - 2 * R - 1; z < zo_begin; ++z)
+#pragma unroll
+        for (int k = 0; k < K1; ++k) add(ld(in, slice, n, z, o1[k]), 1.f);
     typedef float f4 __attribute__((ext_vector_type(4)));
-    auto step = [&](int zc, const float4& e, const float4& l, const float4& c, const float4& v) {
-        acc.x += e.x - l.x + c.x; acc.y += e.y - l.y + c.y;
-        acc.z += e.z - l.z + c.z; acc.w += e.w - l.w + c.w;
+    struct Step {
+        float4 e[K1], l[K1], c[K3], v;
+    };
+    auto load = [&](int zc, Step& s) {
+#pragma unroll
+        for (int k = 0; k < K1; ++k) {
+            s.e[k] = ld(in, slice, n, zc + R, o1[k]);
+            s.l[k] = ld(in, slice, n, zc - R - 1, o1l[k]);
+        }
+#pragma unroll
+        for (int k = 0; k < K3; ++k) s.c[k] = ld(in, slice, n, zc, o3l[k]);
+        s.v = ld(in, slice, n, zc - R, o5l);
+    };
+    auto step = [&](int zc, const Step& s) {
+#pragma unroll
+        for (int k = 0; k < K1; ++k) { add(s.e[k], 1.f); add(s.l[k], -1.f); }
+#pragma unroll
+        for (int k = 0; k < K3; ++k) add(s.c[k], 1.f);
 #if SK_BAR >= 1
         __builtin_amdgcn_s_barrier();
 #endif
         const int zo = zc - R;
         if (zo >= zo_begin) {
+            const float4 v = s.v;
             const float4 w = make_float4(acc.x * v.x, acc.y * v.y, acc.z * v.z, acc.w * v.w);
             if (o5 >= 0) {
                 const f4 wv = {w.x, w.y, w.z, w.w};
@@ -125,30 +152,23 @@ __global__ __launch_bounds__(NT) void skeleton_kernel(const float* __restrict__ 
     };
     const int zc0 = zo_begin - R, zc1 = zo_end + R;  // steps; (zc1 - zc0) % max(SK_PF, 1) == 0
 #if SK_PF == 0
-    for (int zc = zc0; zc < zc1; ++zc)
-        step(zc, ld(in, slice, n, zc + R, o1), ld(in, slice, n, zc - R - 1, o1l),
-             ld(in, slice, n, zc, o3l), ld(in, slice, n, zc - R, o5l));
+    for (int zc = zc0; zc < zc1; ++zc) {
+        Step s;
+        load(zc, s);
+        step(zc, s);
+    }
 #else
     // every load of step zc issued SK_PF steps ahead (slot j of a ring, compile-time index)
     constexpr int D = SK_PF;
-    float4 E[D], L[D], Cq[D], V[D];
+    Step ring[D];
 #pragma unroll
-    for (int j = 0; j < D; ++j) {
-        E[j] = ld(in, slice, n, zc0 + j + R, o1);
-        L[j] = ld(in, slice, n, zc0 + j - R - 1, o1l);
-        Cq[j] = ld(in, slice, n, zc0 + j, o3l);
-        V[j] = ld(in, slice, n, zc0 + j - R, o5l);
-    }
+    for (int j = 0; j < D; ++j) load(zc0 + j, ring[j]);
     for (int zb = zc0; zb < zc1; zb += D) {
 #pragma unroll
         for (int j = 0; j < D; ++j) {
-            const int zc = zb + j, zn = zc + D;
-            const float4 e = E[j], l = L[j], c = Cq[j], v = V[j];
-            E[j] = ld(in, slice, n, zn + R, o1);  // past zc1: harmless extra loads
-            L[j] = ld(in, slice, n, zn - R - 1, o1l);
-            Cq[j] = ld(in, slice, n, zn, o3l);
-            V[j] = ld(in, slice, n, zn - R, o5l);
-            step(zc, e, l, c, v);
+            const Step cur = ring[j];
+            load(zb + j + D, ring[j]);  // past zc1: harmless extra loads
+            step(zb + j, cur);
         }
     }
 #endif
