@@ -169,17 +169,21 @@ def lib_hash() -> str:
     return h.hexdigest()
 
 
-def load_traffic(gshape, radius: int, world: int):
+def load_traffic(gshape, radius: int, world: int, share=None):
     """Per-launch HBM traffic from the committed rocprofv3 PMC summary (profiles/pmc_traffic.json),
-    only when it was measured on this exact library build and workload; else None."""
+    only when it was measured on this exact library build and workload — the same global shape,
+    radius and world size, and for a `--share G/N` proxy the same (G, N) share (entries without a
+    "share" key describe the whole volume); else None."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    want_share = list(share) if share is not None else None
     try:
         with open(path) as f:
             d = json.load(f)
         entries = d.get("entries", [d]) if isinstance(d, dict) else list(d)
         for e in entries:  # one entry per measured workload (G3 r=4, G2 r=2, ...)
             if (e.get("lib_sha256") == lib_hash() and list(e.get("global_shape", [])) == list(gshape)
-                    and e.get("radius") == radius and e.get("world", 1) == world):
+                    and e.get("radius") == radius and e.get("world", 1) == world
+                    and e.get("share") == want_share):
                 return e.get("hbm_bytes_per_launch")
     except (OSError, ValueError, AttributeError):
         pass
@@ -279,7 +283,7 @@ def main():
     ms_per_step = wall * 1000.0 / args.steps
     value = voxels_all * 4 / 2 ** 30 / (ms_per_step / 1000.0)
     achieved = voxels_rank * ALGO_BYTES_PER_VOXEL / (kern_ms / 1000.0) / 1e9  # GB/s per GPU
-    traffic = load_traffic(gshape, radius, world)
+    traffic = load_traffic(gshape, radius, world, share)
 
     headline = share is None and ((size == N and radius == 4 and args.scaling == "strong") or (
         world == 1 and size == N and radius == 4))

@@ -353,6 +353,10 @@ int zt_store_downsample_gaussian(const char* in_path, const char* out_path, cons
                                  zt_store_stats* stats);
 /* 1 if the named codec can be read and written here, else 0. */
 int zt_store_codec_available(const char* name);
+/* Host bytes the store pipeline budgets 80 % of (the available-memory half of
+ * calculate_chunk_limit, filter.rs:52-66): ZT_STORE_HOST_MEMORY if set, else MemAvailable capped
+ * at the cgroup's limit minus its usage net of reclaimable (inactive) page cache. */
+uint64_t zt_store_host_available_bytes(void);
 
 #ifdef __cplusplus
 }

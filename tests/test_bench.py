@@ -66,6 +66,15 @@ def test_traffic_entries_are_keyed_to_build_workload_and_world(monkeypatch, tmp_
     assert bench.load_traffic((1024,) * 3, 2, 1) == 2.0e10
     assert bench.load_traffic((512,) * 3, 2, 1) is None  # measured on another build
     assert bench.load_traffic((2048,) * 3, 4, 2) is None  # another world size
+    # a --share G/N proxy line never carries the whole volume's traffic, only an
+    # entry measured on that share
+    assert bench.load_traffic((2048,) * 3, 4, 1, (3, 8)) is None
+    shared = dict(entries[0], share=[3, 8], hbm_bytes_per_launch=1.9e10)
+    (tmp_path / "profiles" / "pmc_traffic.json").write_text(
+        json.dumps({"entries": entries + [shared]}))
+    assert bench.load_traffic((2048,) * 3, 4, 1, (3, 8)) == 1.9e10
+    assert bench.load_traffic((2048,) * 3, 4, 1, (2, 8)) is None
+    assert bench.load_traffic((2048,) * 3, 4, 1) == 1.0e11
     # the single-entry form of earlier rounds still reads
     (tmp_path / "profiles" / "pmc_traffic.json").write_text(json.dumps(entries[0]))
     assert bench.load_traffic((2048,) * 3, 4, 1) == 1.0e11

@@ -125,3 +125,18 @@ def test_fused_pyramid_levels_equal_per_level_launches(shape, dtype, monkeypatch
         assert g.shape == cur.shape
         np.testing.assert_array_equal(g, cur)
         np.testing.assert_array_equal(g, from_dev(ref, dtype))
+
+
+def test_pyramid_tall_y_beyond_the_fused_grid():
+    """A level-1 y extent past 4 x 65535 rows does not fit the fused launch's grid: those levels
+    take the per-level launches and still equal the oracle's level-by-level result."""
+    import torch
+    shape = (4, 4 * 65536 * 2 + 16, 4)  # level 1 y extent 262152 -> 65538 y workgroups
+    rng = np.random.default_rng(7)
+    v = rng.integers(0, 255, shape, dtype=np.uint8, endpoint=True)
+    levels = zt.pyramid(to_dev(v, "uint8"), (2, 2, 2), max_levels=3)
+    torch.cuda.synchronize()
+    cur = v
+    for lvl in levels:
+        cur = O.downsample(cur, "uint8", (2, 2, 2), "uint8")
+        np.testing.assert_array_equal(from_dev(lvl, "uint8"), cur)

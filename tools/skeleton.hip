@@ -37,10 +37,25 @@
 #ifndef SK_NOP5
 #define SK_NOP5 0
 #endif
+#ifndef SK_STAUX
+#define SK_STAUX 2  // output store cache bits (2 = nt, 16 = sc1: written through, dropped from L2)
+#endif
+#ifndef SK_PADX
+#define SK_PADX 0  // row pitch n + PADX elements
+#endif
+#ifndef SK_PADY
+#define SK_PADY 0  // slice pitch (n + PADY) rows
+#endif
 #ifndef SK_TX
 #define SK_TX 64
 #endif
-constexpr int R = 4, TX = SK_TX, TY = 2048 / SK_TX, NT = 1024, STX = 4, STY = 16;
+#ifndef SK_STX
+#define SK_STX 4
+#endif
+#ifndef SK_STY
+#define SK_STY 16
+#endif
+constexpr int R = 4, TX = SK_TX, TY = 2048 / SK_TX, NT = 1024, STX = SK_STX, STY = SK_STY;
 
 #define CK(x)                                                                              \
     do {                                                                                   \
@@ -71,7 +86,7 @@ __device__ __forceinline__ int apron_off(int q, int x0, int y0, int n) {
     if (q >= QX * QY) return -1;
     const int gx = x0 - M + 4 * (q % QX), gy = y0 - M + q / QX;
     if (gy < 0 || gy >= n || gx < 0 || gx + 3 >= n) return -1;  // n is a multiple of 4
-    return gy * n + gx;
+    return gy * (n + SK_PADX) + gx;
 }
 
 __global__ __launch_bounds__(NT) void skeleton_kernel(const float* __restrict__ in,
@@ -88,7 +103,7 @@ __global__ __launch_bounds__(NT) void skeleton_kernel(const float* __restrict__ 
     const int tile_x = (r / (STX * STY)) * STX + r % STX;
     const int tile_y = sr * STY + (r / STX) % STY;
     const int x0 = tile_x * TX, y0 = tile_y * TY;
-    const long slice = (long)n * n;
+    const long slice = (long)(n + SK_PADX) * (n + SK_PADY);
     const int zo_begin = seg * zseg, zo_end = min(zo_begin + zseg, n);
     const int tid = threadIdx.x;
 
@@ -140,8 +155,12 @@ __global__ __launch_bounds__(NT) void skeleton_kernel(const float* __restrict__ 
             const float4 v = s.v;
             const float4 w = make_float4(acc.x * v.x, acc.y * v.y, acc.z * v.z, acc.w * v.w);
             if (o5 >= 0) {
-                const f4 wv = {w.x, w.y, w.z, w.w};
-                __builtin_nontemporal_store(wv, reinterpret_cast<f4*>(out + (long)zo * slice + o5));
+                typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+                const u4 wv = {__float_as_uint(w.x), __float_as_uint(w.y), __float_as_uint(w.z),
+                               __float_as_uint(w.w)};
+                const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+                    out + (long)zo * slice, (short)0, (int)(slice * 4), 0x00020000);
+                __builtin_amdgcn_raw_buffer_store_b128(wv, ro, o5 * 4, 0, SK_STAUX);
             } else if (w.x == 1.2345e-30f && w.y == -7.5e-31f) {
                 dummy[tid] = w.z + w.w;  // never taken: keeps the apron-only threads' loads live
             }
@@ -190,7 +209,7 @@ int main(int argc, char** argv) {
         fprintf(stderr, "n must be a multiple of %d\n", zseg);
         return 1;
     }
-    const long count = (long)n * n * n;
+    const long count = (long)(n + SK_PADX) * (n + SK_PADY) * n;
     float *in, *out, *dummy;
     CK(hipMalloc(&in, count * 4));
     CK(hipMalloc(&out, count * 4));
@@ -219,8 +238,8 @@ int main(int argc, char** argv) {
         }
     }
     const double gb = (double)count * 8 / 1e9;
-    printf("skeleton SK_BAR=%d SK_PF=%d TX=%d M1=%d noleave=%d noP3=%d noP5=%d lds=%d n=%d wg=%d: mean %.3f ms min %.3f ms (%.1f GB/s algorithmic)\n",
-           SK_BAR, SK_PF, TX, SK_M1, SK_NOLEAVE, SK_NOP3, SK_NOP5, lds, n, nwg, sum / reps, best, gb / (sum / reps) * 1e3);
+    printf("skeleton ST=%dx%d PAD=%d,%d STAUX=%d SK_BAR=%d SK_PF=%d TX=%d M1=%d noleave=%d noP3=%d noP5=%d lds=%d n=%d wg=%d: mean %.3f ms min %.3f ms (%.1f GB/s algorithmic)\n",
+           STX, STY, SK_PADX, SK_PADY, SK_STAUX, SK_BAR, SK_PF, TX, SK_M1, SK_NOLEAVE, SK_NOP3, SK_NOP5, lds, n, nwg, sum / reps, best, gb / (sum / reps) * 1e3);
     CK(hipFree(in));
     CK(hipFree(out));
     CK(hipFree(dummy));

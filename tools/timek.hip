@@ -10,11 +10,7 @@
 #include <cstdlib>
 #include <vector>
 
-#ifdef TK_V4
-#include "gf_v4.hpp"  // schedule experiment (tools/gf_v4.hpp)
-#else
 #include "../zarrs_tools_amd/csrc/gf_fused.hpp"
-#endif
 
 using namespace zt;
 #ifndef TK_TY

@@ -193,6 +193,7 @@ def lib() -> ctypes.CDLL:
                                           ctypes.c_char_p, c_int, ctypes.c_int64, ctypes.c_int64,
                                           c_int, c_int, ctypes.POINTER(StoreStats)], c_int),
         "zt_store_codec_available": ([ctypes.c_char_p], c_int),
+        "zt_store_host_available_bytes": ([], ctypes.c_uint64),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

@@ -265,7 +265,7 @@ static hipError_t launch_pyr_fused_t(const void* in, void* const* outs, const Py
     // z capped at 128 workgroup layers, each workgroup looping over level-1 z blocks: 4096^3 u16
     // levels 1-3 in 29.2 ms against 31.8 ms for one layer per z block (tools/timepyr.hip)
     const int64_t gz = std::min<int64_t>((p.s[1][0] + 3) / 4, 128);
-    if (gx > 0x7FFFFFFF || gy > 65535) return hipErrorInvalidValue;
+    if (gx > 0x7FFFFFFF || gy > 65535) return hipErrorInvalidValue;  // pyramid_fused_grid_fits
     const bool vec = p.s[0][2] % 8 == 0 && (uintptr_t)in % (8 * sizeof(T)) == 0 &&
                      (uintptr_t)outs[0] % (4 * sizeof(T)) == 0;
     const dim3 grid((unsigned)gx, (unsigned)gy, (unsigned)gz);
@@ -281,6 +281,10 @@ static hipError_t launch_pyr_fused_t(const void* in, void* const* outs, const Py
         else hipLaunchKernelGGL((pyramid3_fused_kernel<T, 2, false>), grid, dim3(256), 0, s, i, o1, o2, o3, p);
     }
     return hipGetLastError();
+}
+
+bool pyramid_fused_grid_fits(const int64_t* s1) {
+    return (s1[2] + 255) / 256 <= 0x7FFFFFFF && (s1[1] + 3) / 4 <= 65535;
 }
 
 bool pyramid_fused_dtype(int dtype) {

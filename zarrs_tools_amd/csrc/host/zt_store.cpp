@@ -484,9 +484,29 @@ bool read_cgroup_u64(const char* path, uint64_t& v) {
     return true;
 }
 
+// "key value" from a cgroup memory.stat file.
+bool read_stat_key(const std::string& path, const char* key, uint64_t& v) {
+    FILE* f = std::fopen(path.c_str(), "r");
+    if (!f) return false;
+    char line[256];
+    bool found = false;
+    const size_t kl = std::strlen(key);
+    while (std::fgets(line, sizeof line, f)) {
+        if (std::strncmp(line, key, kl) == 0 && line[kl] == ' ') {
+            v = std::strtoull(line + kl + 1, nullptr, 10);
+            found = true;
+            break;
+        }
+    }
+    std::fclose(f);
+    return found;
+}
+
 uint64_t host_available_bytes() {
     if (const char* e = std::getenv("ZT_STORE_HOST_MEMORY")) return std::strtoull(e, nullptr, 10);
-    FILE* f = std::fopen("/proc/meminfo", "r");
+    // ZT_MEMINFO / ZT_CGROUP_ROOT relocate the files read below (tests)
+    const char* mi = std::getenv("ZT_MEMINFO");
+    FILE* f = std::fopen(mi ? mi : "/proc/meminfo", "r");
     uint64_t kb = 0;
     if (f) {
         char line[256];
@@ -496,13 +516,27 @@ uint64_t host_available_bytes() {
     }
     uint64_t avail = kb ? kb * 1024 : (uint64_t)16 << 30;
     // Inside a memory-limited cgroup MemAvailable describes the whole machine: cap it at the
-    // cgroup's limit minus its usage (v2: memory.max / memory.current, v1: limit / usage).
-    uint64_t lim = 0, use = 0;
-    if ((read_cgroup_u64("/sys/fs/cgroup/memory.max", lim) &&
-         read_cgroup_u64("/sys/fs/cgroup/memory.current", use)) ||
-        (read_cgroup_u64("/sys/fs/cgroup/memory/memory.limit_in_bytes", lim) &&
-         read_cgroup_u64("/sys/fs/cgroup/memory/memory.usage_in_bytes", use))) {
-        if (lim < ((uint64_t)1 << 60)) avail = std::min(avail, lim > use ? lim - use : 0);
+    // cgroup's limit minus its usage (v2: memory.max / memory.current, v1: limit / usage). The
+    // usage counts page cache, which the kernel reclaims on demand (a store pipeline that has just
+    // read or written GBs of chunks sits near its limit on cache alone), so the inactive file
+    // pages (memory.stat inactive_file / total_inactive_file) are subtracted from it, as
+    // MemAvailable counts reclaimable cache as available.
+    const char* cr = std::getenv("ZT_CGROUP_ROOT");
+    const std::string root = cr ? cr : "/sys/fs/cgroup";
+    uint64_t lim = 0, use = 0, inact = 0;
+    bool got = false;
+    if (read_cgroup_u64((root + "/memory.max").c_str(), lim) &&
+        read_cgroup_u64((root + "/memory.current").c_str(), use)) {
+        got = true;
+        if (!read_stat_key(root + "/memory.stat", "inactive_file", inact)) inact = 0;
+    } else if (read_cgroup_u64((root + "/memory/memory.limit_in_bytes").c_str(), lim) &&
+               read_cgroup_u64((root + "/memory/memory.usage_in_bytes").c_str(), use)) {
+        got = true;
+        if (!read_stat_key(root + "/memory/memory.stat", "total_inactive_file", inact)) inact = 0;
+    }
+    if (got && lim < ((uint64_t)1 << 60)) {
+        const uint64_t used = use > inact ? use - inact : 0;
+        avail = std::min(avail, lim > used ? lim - used : 0);
     }
     return avail;
 }
@@ -1236,6 +1270,8 @@ int zt_store_set_chunk_limit(int64_t max_chunks) {
     g_chunk_limit = max_chunks;
     return ZT_OK;
 }
+
+uint64_t zt_store_host_available_bytes(void) { return host_available_bytes(); }
 
 int zt_store_codec_available(const char* name) {
     if (!name) return 0;

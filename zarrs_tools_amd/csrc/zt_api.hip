@@ -1084,6 +1084,9 @@ int zt_pyramid_downsample(zt_ctx* ctx, int dtype, const void* level0, const int6
             if (sh[0] < 2 || sh[1] < 2 || sh[2] < 2) break;
             ++k;
         }
+        // the fused grid's y extent covers level-1 rows in fours: past 65535 workgroups (an
+        // input y extent of ~524k) the levels run one launch each instead
+        if (k >= 2 && !zt::pyramid_fused_grid_fits(level_shape(i + 1))) k = 0;
         if (k >= 2) {
             int64_t sh3[4][3] = {};
             for (int l = 0; l <= k; ++l) std::copy(level_shape(i + l), level_shape(i + l) + 3, sh3[l]);

@@ -192,13 +192,15 @@ def create_output(input_path, output_path, data_type: Optional[str] = None, shap
 
 def host_available_bytes() -> int:
     """Host memory the store pipeline may budget (as host_available_bytes in host/zt_store.cpp):
-    ZT_STORE_HOST_MEMORY if set, else MemAvailable capped at the cgroup's limit minus its usage."""
+    ZT_STORE_HOST_MEMORY if set, else MemAvailable capped at the cgroup's limit minus its usage,
+    the usage without the cgroup's inactive file pages (reclaimable page cache, which MemAvailable
+    counts as available). ZT_MEMINFO / ZT_CGROUP_ROOT relocate the files read (tests)."""
     env = os.environ.get("ZT_STORE_HOST_MEMORY")
     if env:
         return int(env)
     avail = 16 << 30
     try:
-        with open("/proc/meminfo") as f:
+        with open(os.environ.get("ZT_MEMINFO", "/proc/meminfo")) as f:
             for line in f:
                 if line.startswith("MemAvailable:"):
                     avail = int(line.split()[1]) * 1024
@@ -214,13 +216,27 @@ def host_available_bytes() -> int:
         except OSError:
             return None
 
-    for lim_p, use_p in (("/sys/fs/cgroup/memory.max", "/sys/fs/cgroup/memory.current"),
-                         ("/sys/fs/cgroup/memory/memory.limit_in_bytes",
-                          "/sys/fs/cgroup/memory/memory.usage_in_bytes")):
-        lim, use = _u64(lim_p), _u64(use_p)
+    def _stat(path, key):
+        try:
+            with open(path) as f:
+                for line in f:
+                    k, _, v = line.partition(" ")
+                    if k == key:
+                        return int(v)
+        except (OSError, ValueError):
+            pass
+        return 0
+
+    root = os.environ.get("ZT_CGROUP_ROOT", "/sys/fs/cgroup")
+    for lim_p, use_p, stat_p, key in (
+            ("memory.max", "memory.current", "memory.stat", "inactive_file"),
+            ("memory/memory.limit_in_bytes", "memory/memory.usage_in_bytes",
+             "memory/memory.stat", "total_inactive_file")):
+        lim, use = _u64(os.path.join(root, lim_p)), _u64(os.path.join(root, use_p))
         if lim is not None and use is not None:
             if lim < (1 << 60):
-                avail = min(avail, max(0, lim - use))
+                used = max(0, use - _stat(os.path.join(root, stat_p), key))
+                avail = min(avail, max(0, lim - used))
             break
     return avail
 

@@ -235,6 +235,19 @@ def _nbytes(shape, data_type) -> int:
     return n * S.NUMPY[data_type]().itemsize
 
 
+def allocation_refused(e: BaseException) -> bool:
+    """True for a refused device or pinned-host allocation (the callers then fall back to the
+    store -> store path); False for everything else, FilterError (storage, codecs) included."""
+    import torch
+    if isinstance(e, _abi.FilterError):
+        return False
+    if isinstance(e, torch.cuda.OutOfMemoryError):
+        return True
+    msg = str(e).lower()
+    return isinstance(e, RuntimeError) and ("out of memory" in msg or "pinned" in msg or
+                                            "hiphostmalloc" in msg or "cudahostalloc" in msg)
+
+
 def read_to_device(path, device: int, nthreads: int = 0):
     """A whole store array decoded straight into pinned host memory and copied to the device at
     pinned-transfer speed; bfloat16 arrays come back as torch.bfloat16."""
@@ -287,19 +300,22 @@ def run_device_chain(steps: list, paths: list, device: int = 0, nthreads: int = 
     if host_need > budget_frac * S.host_available_bytes():
         return None
     results = []
-    for k, step in enumerate(steps):
-        f, src_info, oshape, odt = plan[k]
-        S.create_output(paths[k], paths[k + 1], odt, oshape, encoding_of(step))
-    # The last output is "not finished" (no zarr.json, zarrs_filter.rs:297-313) until its chunks
-    # are written; a failing step leaves no output that looks complete.
-    S.hold_metadata(paths[-1])
     t0 = time.perf_counter()
     src_info = S.open_array(paths[0])
     try:
         x = read_to_device(paths[0], device, nthreads)
-    except RuntimeError:  # pinned host or device allocation refused: the store path instead
-        return None
+    except RuntimeError as e:
+        if not allocation_refused(e):
+            raise  # storage / codec errors (FilterError) are real failures
+        return None  # pinned host or device allocation refused: the store path instead
     t_read = time.perf_counter() - t0
+    for k, step in enumerate(steps):
+        f, src_info_k, oshape, odt = plan[k]
+        S.create_output(paths[k], paths[k + 1], odt, oshape, encoding_of(step))
+    # The last output is "not finished" (no zarr.json, zarrs_filter.rs:297-313) until its chunks
+    # are written; a failing step leaves no output that looks complete. Held only once the input
+    # is on the device, so a fallback to the store path never leaves a stale pending file.
+    S.hold_metadata(paths[-1])
     dev = torch.device("cuda", device)
     x_dt, x_chunk = src_info.data_type, src_info.chunk_shape
     ctx = F.default_context(device)

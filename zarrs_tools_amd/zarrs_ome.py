@@ -47,8 +47,8 @@ import numpy as np
 
 from . import _abi
 from . import store as S
-from .zarrs_filter import (REENCODE_KEYS, _add_reencode_args, _device_ok, encoding_of,
-                           read_to_device, write_from_device)
+from .zarrs_filter import (REENCODE_KEYS, _add_reencode_args, _device_ok, allocation_refused,
+                           encoding_of, read_to_device, write_from_device)
 
 VERSION = "zarrs_tools_amd 0.2 (MI355X)"
 
@@ -423,10 +423,11 @@ def run(input_path, output_path, factor=None, max_levels: int = 10, discrete: bo
         boxes = [shard.octant_assignment(g, gpus, shape, factor, len(level_shapes))
                  for g in range(gpus)]
         big = max(boxes, key=lambda b: int(np.prod(b.shape)))
-        sharing = max(devices.count(d) for d in devices)
         box_info = S.ArrayInfo(lvl0, lvl0_info.data_type, tuple(big.shape), (), ())
-        if big.local_levels > 0 and _device_pyramid_fits(box_info, None, devices[0],
-                                                         sharing=sharing, host_share=gpus):
+        # every distinct device must hold its processes' boxes (each with its own count)
+        fits = all(_device_pyramid_fits(box_info, None, d, sharing=devices.count(d),
+                                        host_share=gpus) for d in sorted(set(devices)))
+        if big.local_levels > 0 and fits:
             prepare_octant_levels(output_path, level_shapes, big.local_levels)
             octants_done, st_oct = run_octants(output_path, shape, factor, len(level_shapes),
                                                discrete, gpus, devices, nthreads, log)
@@ -441,8 +442,10 @@ def run(input_path, output_path, factor=None, max_levels: int = 10, discrete: bo
         t1 = time.perf_counter()
         try:
             cur = read_to_device(lvl0, device, nthreads)
-        except RuntimeError:  # pinned host or device allocation refused: the store path
-            on_device = False
+        except RuntimeError as e:
+            if not allocation_refused(e):
+                raise  # storage / codec errors are real failures
+            on_device = False  # pinned host or device allocation refused: the store path
         log(f"   level 0 -> device in {time.perf_counter() - t1:.2f}s")
     for i in range(1, len(level_shapes) + 1):
         src, dst = os.path.join(output_path, str(i - 1)), os.path.join(output_path, str(i))
