@@ -129,44 +129,64 @@ def bench_guided4d(shape, chunk, radius, reps):
                              "guided filter (C restatement of guided_filter.rs)"}}
 
 
-def bench_t_share(reps, radius=2):
-    """Config T's real per-GPU share (SURVEY.md §8(e), rows along t): output timepoints [8, 12)
-    of the (32, 1024^3) f32 series, computed from the rank's (12, 1024^3) input block (the 2r
-    t-halo) generated from the global synthetic definition; the chunk grid of the block's middle
-    row (64 chunks of (4, 256^3)) through GuidedFilter::apply's per-chunk path. Algorithmic bytes:
-    8 per OUTPUT voxel (the t-halo reads are not credited)."""
+def bench_t_share(reps, radius=2, groups=None, rank=None):
+    """Config T's real per-GPU share: rank `rank` of an 8-GPU split of the
+    (32, 1024^3) f32 series in (4, 256^3) chunks, timed alone on this GPU. The chunk grid is
+    split in (t, z) blocks of whole chunks (shard.block_assignment; `groups` = (t groups, z groups),
+    default the input-minimising 2 x 4: 16 output timepoints x 256 planes from a 20 x 264-plane
+    input, 1.29x stage-1 work, where rows along t (8 x 1) read 12 timepoints for 4, 3x). The
+    rank's halo'd input block is generated from the global synthetic definition and filtered in
+    one GuidedFilter::apply_ndarray call on its output box (chunked == whole with the 2r halo,
+    SURVEY.md §0.2). Algorithmic bytes: 8 per OUTPUT voxel (halo reads not credited)."""
     import numpy as np
     import torch
     import zarrs_tools_amd as zt
+    from zarrs_tools_amd import shard
+    from zarrs_tools_amd.filter import ArraySubset
     from oracle import oracle as O
     ctx = zt.default_context(0)
-    gshape, chunk, t0, tin = (32, 1024, 1024, 1024), (4, 256, 256, 256), 4, 12
-    x = zt.synth_box((t0, 0, 0, 0), (tin,) + gshape[1:], gshape, kind="float32", ctx=ctx)
-    y = torch.zeros_like(x)
+    gshape, chunk, world = (32, 1024, 1024, 1024), (4, 256, 256, 256), 8
+    halo = 2 * radius
+    groups = tuple(groups) if groups else shard.block_split(world, gshape, chunk, halo)
+    if rank is None:  # an interior block (largest input)
+        rank = (groups[0] // 2) * groups[1] + groups[1] // 2 if groups[1] > 1 else groups[0] // 2
+    a = shard.block_assignment(rank, world, gshape, chunk, halo, groups)
+    x = zt.synth_box(a.in_start, a.in_shape, gshape, kind="float32", ctx=ctx)
+    rel0 = tuple(o - i for o, i in zip(a.out_start, a.in_start))
     g = zt.GuidedFilter(2500.0, radius)
-    a_in, a_out = zt.DeviceArray(x, chunk), zt.DeviceArray(y, chunk)
-    ms = timed(lambda: g.apply(a_in, a_out, ctx=ctx, chunk_grid_start=(1, 0, 0, 0),
-                               chunk_grid_count=(1, 4, 4, 4)),
-               torch.cuda.current_stream(), reps)
-    n = 4 * 1024 ** 3
+    sub = ArraySubset(rel0, a.out_shape)
+    res = {}
+
+    def run():
+        res["y"] = None  # drop the previous output first (the caching allocator reuses it)
+        res["y"] = g.apply_ndarray(x, sub, ctx=ctx)
+
+    ms = timed(run, torch.cuda.current_stream(), reps)
+    y = res["y"]
+    n = int(np.prod(a.out_shape))
     gbs = n * 8 / (ms / 1e3) / 1e9
     # parity: one interior chunk of the share against the oracle's per-chunk result
-    (o0, osh, ref), = O.guided_filter_synth_chunks(gshape, chunk, [(2, 1, 2, 3)], 2500.0, radius,
+    cidx = tuple((o + s // 2) // c for o, s, c in zip(a.out_start, a.out_shape, chunk))
+    (o0, osh, ref), = O.guided_filter_synth_chunks(gshape, chunk, [cidx], 2500.0, radius,
                                                    nthreads=16)
-    got = y[o0[0] - t0:o0[0] - t0 + 4, o0[1]:o0[1] + 256, o0[2]:o0[2] + 256,
-            o0[3]:o0[3] + 256].cpu().numpy()
+    sl = tuple(slice(p - q, p - q + s) for p, q, s in zip(o0, a.out_start, osh))
+    got = y[sl].cpu().numpy()
     rel = float((np.abs(got.astype(np.float64) - ref) / np.maximum(1.0, np.abs(ref))).max())
-    del x, y
+    del x, y, res
+    ctx.release_scratch()
     torch.cuda.empty_cache()
     return {"op": f"guided_filter r={radius} 4-D, config T per-GPU share (device-resident)",
-            "config": {"global_shape": list(gshape), "input_block_t": [t0, t0 + tin],
-                       "output_t": [t0 + 4, t0 + 8], "dtype": "float32", "chunk": list(chunk),
-                       "eps": 2500.0, "path": "per chunk (12, 264^3) input, four-kernel 4-D"},
+            "config": {"global_shape": list(gshape), "chunk": list(chunk), "world": world,
+                       "groups_t_z": list(groups), "rank": rank,
+                       "output_box": [list(a.out_start), list(a.out_shape)],
+                       "input_box": [list(a.in_start), list(a.in_shape)],
+                       "dtype": "float32", "eps": 2500.0,
+                       "path": "one apply_ndarray call on the halo'd (t, z) block, four-kernel 4-D"},
             "ms": round(ms, 4), "gib_per_s": round(n * 4 / 2 ** 30 / (ms / 1e3), 3),
             "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
                          "algorithmic_bytes": n * 8},
-            "parity_max_rel": rel}
+            "parity_chunk": list(cidx), "parity_max_rel": rel}
 
 
 def main():
@@ -177,10 +197,13 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--t-shape", type=int, nargs=4, default=[4, 1024, 1024, 1024])
     ap.add_argument("--only", default="pyramid,gaussian,tshare")
+    ap.add_argument("--t-groups", type=int, nargs=2, default=None,
+                    help="config T share: (t groups, z groups) of the 8-GPU split")
+    ap.add_argument("--t-rank", type=int, default=None)
     a = ap.parse_args()
     only = set(a.only.split(","))
     if "tshare" in only:
-        print(json.dumps(bench_t_share(a.reps)), flush=True)
+        print(json.dumps(bench_t_share(a.reps, groups=a.t_groups, rank=a.t_rank)), flush=True)
     if "guided4d" in only:
         print(json.dumps(bench_guided4d(a.t_shape, (4, 256, 256, 256), 2, a.reps)), flush=True)
         if only == {"guided4d"}:

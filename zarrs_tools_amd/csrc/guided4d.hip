@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "zt_device.hpp"
 #include "zt_kernels.hpp"
@@ -254,6 +255,97 @@ __global__ __launch_bounds__(256) void g4_final_kernel(const float2* __restrict_
     }
 }
 
+// K2 / K4 for blocks of up to TMAX = 32 timepoints (config T's (t, z) block shares: 16 output
+// timepoints plus the 2r halo): the t-window sums slide along t in registers (the radius R a
+// template parameter, so the entering and leaving timepoints are compile-time register indices)
+// instead of one masked sum per output timepoint (O(T) instead of O(T^2) adds per voxel). Values
+// past T are zero, so the running window stays exact (f64 sums of f64 / f32 values).
+template <int TMAX, int R>
+__global__ __launch_bounds__(256) void g4_pointwise_slide_kernel(const double* __restrict__ U3,
+                                                                 const float* __restrict__ v,
+                                                                 float2* __restrict__ AB, int T,
+                                                                 int ta_ab, int tb_ab, int nz,
+                                                                 int ny, int nx, float eps,
+                                                                 Str3 vs) {
+    const int64_t vol = (int64_t)nz * ny * nx;
+    const int x = blockIdx.x * kPX + threadIdx.x, y = blockIdx.y * kPY + threadIdx.y;
+    if (x >= nx || y >= ny) return;
+    const int cyx = ccount(y, ny, R) * ccount(x, nx, R);
+    for (int z = blockIdx.z; z < nz; z += gridDim.z) {
+        const int64_t i = ((int64_t)z * ny + y) * nx + x;
+        const int c3 = ccount(z, nz, R) * cyx;
+        double U[TMAX];
+#pragma unroll
+        for (int t = 0; t < TMAX; ++t) U[t] = t < T ? U3[t * vol + i] : 0.0;
+        double W = 0.0;  // window of t = 0: [0, R]
+#pragma unroll
+        for (int j = 0; j <= R && j < TMAX; ++j) W += U[j];
+#pragma unroll
+        for (int t = 0; t < TMAX; ++t) {
+            if (t > 0) {
+                if (t + R < TMAX) W += U[t + R];
+                if (t - R - 1 >= 0) W -= U[t - R - 1];
+            }
+            if (t >= T || t < ta_ab || t >= tb_ab) continue;  // only the (a, b) K4 reads
+            const int ta = max(t - R, 0), tb = min(t + R, T - 1);
+            const float cnt = (float)(c3 * (tb - ta + 1));
+            const float u = (float)W / cnt;  // summed_area_table_mean: (sum as f32) / count
+            const float d = v[t * vs.t + (int64_t)z * vs.z + (int64_t)y * vs.y + x] - u;
+            const float sq = d * d;  // (v - u).powf(2.0)
+            const float a = sq / (sq + eps);
+            const float b = (1.0f - a) * u;
+            AB[t * vol + i] = make_float2(a, b);
+        }
+    }
+}
+
+template <int TMAX, int R, typename TOut>
+__global__ __launch_bounds__(256) void g4_final_slide_kernel(const float2* __restrict__ S3,
+                                                             const float* __restrict__ v,
+                                                             TOut* __restrict__ out, NdGeom g,
+                                                             Str3 vs) {
+    const int T = (int)g.shape[0], nz = (int)g.shape[1], ny = (int)g.shape[2],
+              nx = (int)g.shape[3];
+    const int64_t vol = (int64_t)nz * ny * nx;
+    const int ox = blockIdx.x * kPX + threadIdx.x, oy = blockIdx.y * kPY + threadIdx.y;
+    if (ox >= (int)g.out_shape[3] || oy >= (int)g.out_shape[2]) return;
+    const int x = ox + (int)g.out_start[3], y = oy + (int)g.out_start[2];
+    const int cyx = ccount(y, ny, R) * ccount(x, nx, R);
+    const int t0 = (int)g.out_start[0], ont = (int)g.out_shape[0];
+    const int tlo = max(t0 - R, 0), thi = min(t0 + ont + R, T);
+    for (int oz = blockIdx.z; oz < (int)g.out_shape[1]; oz += gridDim.z) {
+        const int z = oz + (int)g.out_start[1];
+        const int64_t bi = ((int64_t)z * ny + y) * nx + x;
+        const int c3 = ccount(z, nz, R) * cyx;
+        const int64_t dbase = oz * g.out_strides[1] + oy * g.out_strides[2] + ox * g.out_strides[3];
+        float2 S[TMAX];
+#pragma unroll
+        for (int t = 0; t < TMAX; ++t)
+            S[t] = t >= tlo && t < thi ? S3[t * vol + bi] : make_float2(0.f, 0.f);
+        double sa = 0.0, sb = 0.0;  // window of t = 0
+#pragma unroll
+        for (int j = 0; j <= R && j < TMAX; ++j) {
+            sa += (double)S[j].x;
+            sb += (double)S[j].y;
+        }
+#pragma unroll
+        for (int t = 0; t < TMAX; ++t) {
+            if (t > 0) {
+                if (t + R < TMAX) { sa += (double)S[t + R].x; sb += (double)S[t + R].y; }
+                if (t - R - 1 >= 0) { sa -= (double)S[t - R - 1].x; sb -= (double)S[t - R - 1].y; }
+            }
+            const int ot = t - t0;
+            if (ot < 0 || ot >= ont || t >= T) continue;
+            const int ta = max(t - R, 0), tb = min(t + R, T - 1);
+            const float cnt = (float)(c3 * (tb - ta + 1));
+            const float ma = (float)sa / cnt, mb = (float)sb / cnt;
+            const float vv = v[t * vs.t + (int64_t)z * vs.z + (int64_t)y * vs.y + x];
+            const float o = __fadd_rn(__fmul_rn(vv, ma), mb);  // v *= ma; v += mb
+            out[dbase + ot * g.out_strides[0]] = from_f32<TOut>(o);
+        }
+    }
+}
+
 template <int R, typename TV, typename TA, typename TO>
 hipError_t launch_box3(const TV* in, TO* out, int T, int nz, int ny, int nx, Str3 is,
                        hipStream_t s) {
@@ -286,7 +378,7 @@ hipError_t launch_box3_r(int r, const TV* in, TO* out, int T, int nz, int ny, in
 
 }  // namespace
 
-// radius <= 6: the f64-pair LDS tiles of K3 stay within 64 KB; T <= 16 and ny <= 65535 are
+// radius <= 6: the f64-pair LDS tiles of K3 stay within 64 KB; T <= 32 and ny <= 65535 are
 // checked by the caller (K2 / K4 hold a voxel's timepoints in registers, y is grid.y)
 bool guided4d_supports(int radius) { return radius >= 1 && radius <= 6; }
 
@@ -339,7 +431,18 @@ hipError_t launch_guided4d(const void* in, int dtype_in, void* out, int dtype_ou
     else if (T <= 16)
         hipLaunchKernelGGL(g4_pointwise_kernel<16>, pgrid, pblock, 0, s, U3, v, AB, T, ta_ab,
                            tb_ab, nz, ny, nx, radius, eps, vs);
-    else
+    else if (T <= 32) {  // config T's (t, z) block shares: 16 output timepoints + the 2r halo
+        switch (radius) {
+#define ZT_G4_K2(RR)                                                                              \
+    case RR:                                                                                      \
+        hipLaunchKernelGGL((g4_pointwise_slide_kernel<32, RR>), pgrid, pblock, 0, s, U3, v, AB, T, \
+                           ta_ab, tb_ab, nz, ny, nx, eps, vs);                                    \
+        break;
+        ZT_G4_K2(1) ZT_G4_K2(2) ZT_G4_K2(3) ZT_G4_K2(4) ZT_G4_K2(5) ZT_G4_K2(6)
+#undef ZT_G4_K2
+        default: return hipErrorInvalidValue;
+        }
+    } else
         return hipErrorInvalidValue;
     if ((e = hipGetLastError()) != hipSuccess) return e;
     float2* S3 = reinterpret_cast<float2*>(U3);
@@ -360,11 +463,28 @@ hipError_t launch_guided4d(const void* in, int dtype_in, void* out, int dtype_ou
             hipLaunchKernelGGL((g4_final_kernel<4, TO>), fgrid, dim3(kPX, kPY), 0, s, S3, v,
                                static_cast<TO*>(out), g, radius, vs);
             e = hipGetLastError())
-    } else {
+    } else if (T <= 16) {
         ZT_DISPATCH_DTYPE(dtype_out, TO,
             hipLaunchKernelGGL((g4_final_kernel<16, TO>), fgrid, dim3(kPX, kPY), 0, s, S3, v,
                                static_cast<TO*>(out), g, radius, vs);
             e = hipGetLastError())
+    } else {
+        auto launch = [&](auto rr) {
+            constexpr int RR = decltype(rr)::value;
+            ZT_DISPATCH_DTYPE(dtype_out, TO,
+                hipLaunchKernelGGL((g4_final_slide_kernel<32, RR, TO>), fgrid, dim3(kPX, kPY), 0,
+                                   s, S3, v, static_cast<TO*>(out), g, vs);
+                e = hipGetLastError())
+        };
+        switch (radius) {
+        case 1: launch(std::integral_constant<int, 1>{}); break;
+        case 2: launch(std::integral_constant<int, 2>{}); break;
+        case 3: launch(std::integral_constant<int, 3>{}); break;
+        case 4: launch(std::integral_constant<int, 4>{}); break;
+        case 5: launch(std::integral_constant<int, 5>{}); break;
+        case 6: launch(std::integral_constant<int, 6>{}); break;
+        default: return hipErrorInvalidValue;
+        }
     }
     return e;
 }

@@ -298,7 +298,7 @@ int run_separable(zt_ctx* ctx, int dtype_in, const void* in, const int64_t* shap
 // 4-D blocks (config T): guided4d.hip when the radius fits it and x is the unit-stride axis;
 // the scratch holds U3/S3, AB and (for other element types or strides) f32 v.
 bool use_guided4d(int ndim, int radius, const int64_t* in_strides, const int64_t* shape) {
-    return ndim == 4 && zt::guided4d_supports(radius) && in_strides[3] == 1 && shape[0] <= 16 &&
+    return ndim == 4 && zt::guided4d_supports(radius) && in_strides[3] == 1 && shape[0] <= 32 &&
            shape[1] <= 0x7FFFFFFF && shape[2] <= 65535 && shape[3] <= 0x7FFFFFFF;
 }
 

@@ -163,3 +163,79 @@ def assemble_chunk(chunk_start, chunk_shape, pieces):
         src = tuple(slice(l - b, h - b) for l, h, b in zip(lo, hi, bstart))
         out[dst] = arr[src]
     return out
+
+
+@dataclass(frozen=True)
+class BlockAssignment:
+    """Rank `rank`'s box of whole output chunks over the two leading axes (all of the others),
+    and the input box it reads: the output box plus the halo on axes 0 and 1, clamped."""
+    rank: int
+    world: int
+    groups: tuple          # (g0, g1): ranks along axis 0 and axis 1
+    out_start: tuple
+    out_shape: tuple
+    in_start: tuple
+    in_shape: tuple
+
+
+def _split(n_chunks: int, parts: int, k: int) -> tuple:
+    return k * n_chunks // parts, (k + 1) * n_chunks // parts
+
+
+def block_split(world: int, shape, chunk_shape, halo: int) -> tuple:
+    """(g0, g1) with g0 * g1 == world that minimises the input the ranks read in all — the
+    stage-1 work, since every rank recomputes its halo (config T, SURVEY.md §8(e): a t-only split
+    of a (32, 1024^3) series in (4, 256^3) chunks reads 12 timepoints for 4 output ones, 3x; a
+    (t, z) split of 4 x 2 reads 12 x 520 planes per 8 x 512 outputs, 1.5x). Ties: fewer groups
+    along axis 1."""
+    n0 = -(-shape[0] // chunk_shape[0])
+    n1 = -(-shape[1] // chunk_shape[1]) if len(shape) > 1 else 1
+    best = None
+    for g0 in range(1, world + 1):
+        if world % g0:
+            continue
+        g1 = world // g0
+        if g0 > n0 or g1 > n1:
+            continue
+        total = 0
+        for k0 in range(g0):
+            c0, c1 = _split(n0, g0, k0)
+            a0, b0 = c0 * chunk_shape[0], min(c1 * chunk_shape[0], shape[0])
+            e0 = min(b0 + halo, shape[0]) - max(a0 - halo, 0)
+            for k1 in range(g1):
+                d0, d1 = _split(n1, g1, k1)
+                a1, b1 = d0 * chunk_shape[1], min(d1 * chunk_shape[1], shape[1])
+                e1 = min(b1 + halo, shape[1]) - max(a1 - halo, 0)
+                total += e0 * e1
+        key = (total, g1)
+        if best is None or key < best[0]:
+            best = (key, (g0, g1))
+    return best[1] if best else (world, 1)
+
+
+def block_assignment(rank: int, world: int, shape, chunk_shape, halo: int,
+                     groups=None) -> BlockAssignment:
+    """Rank `rank` of `world`: its (axis-0, axis-1) box of whole output chunks (groups from
+    block_split unless given) and the halo'd input box (ArraySubsetOverlap,
+    array_subset_overlap.rs:11-35, on the box instead of each chunk)."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError("bad rank/world")
+    g0, g1 = groups or block_split(world, shape, chunk_shape, halo)
+    if g0 * g1 != world:
+        raise ValueError("groups must multiply to world")
+    nd = len(shape)
+    n0 = -(-shape[0] // chunk_shape[0])
+    n1 = -(-shape[1] // chunk_shape[1])
+    k0, k1 = rank // g1, rank % g1
+    c0, c1 = _split(n0, g0, k0)
+    d0, d1 = _split(n1, g1, k1)
+    a0, b0 = min(c0 * chunk_shape[0], shape[0]), min(c1 * chunk_shape[0], shape[0])
+    a1, b1 = min(d0 * chunk_shape[1], shape[1]), min(d1 * chunk_shape[1], shape[1])
+    out_start = (a0, a1) + (0,) * (nd - 2)
+    out_shape = (b0 - a0, b1 - a1) + tuple(shape[2:])
+    i0, i1 = max(a0 - halo, 0), max(a1 - halo, 0)
+    in_start = (i0, i1) + (0,) * (nd - 2)
+    in_shape = (min(b0 + halo, shape[0]) - i0, min(b1 + halo, shape[1]) - i1) + tuple(shape[2:])
+    if b0 <= a0 or b1 <= a1:
+        in_shape = (0,) * nd
+    return BlockAssignment(rank, world, (g0, g1), out_start, out_shape, in_start, in_shape)

@@ -48,6 +48,8 @@ import sys
 import tempfile
 import time
 
+import numpy as np
+
 from . import _abi
 from . import store as S
 
@@ -248,29 +250,98 @@ def allocation_refused(e: BaseException) -> bool:
                                             "hiphostmalloc" in msg or "cudahostalloc" in msg)
 
 
-def read_to_device(path, device: int, nthreads: int = 0):
-    """A whole store array decoded straight into pinned host memory and copied to the device at
-    pinned-transfer speed; bfloat16 arrays come back as torch.bfloat16."""
+def _row_spans(start0: int, n0: int, chunk0: int) -> list:
+    """[a, b) pieces of the axis-0 range [start0, start0 + n0) cut at the chunk grid, so that
+    every chunk (or shard) is decoded / encoded by one piece only."""
+    spans, a, end = [], start0, start0 + n0
+    while a < end:
+        b = min((a // chunk0 + 1) * chunk0, end)
+        spans.append((a, b))
+        a = b
+    return spans
+
+
+def read_to_device(path, device: int, nthreads: int = 0, start=None, shape=None):
+    """The box [start, start + shape) of a store array (the whole array by default) decoded into
+    HBM, overlapped chunk row by chunk row: a host thread decodes row k+1
+    into one of three pinned row buffers while row k is copied host-to-device on a side stream
+    (the reference copies level 0 then streams it chunk by chunk, zarrs_ome.rs:341-366,
+    631-714). Each chunk is decoded once. bfloat16 arrays come back as torch.bfloat16."""
     import torch
+    from concurrent.futures import ThreadPoolExecutor
     from . import filter as F
     info = S.open_array(path)
+    nd = info.ndim
+    start = [0] * nd if start is None else [int(v) for v in start]
+    shape = list(info.shape) if shape is None else [int(v) for v in shape]
     store_dt = "uint16" if info.data_type == "bfloat16" else info.data_type
-    host = torch.empty(tuple(info.shape), dtype=F.torch_dtype(store_dt), pin_memory=True)
-    S.read_array(path, nthreads=nthreads, out=host.numpy())
-    x = host.to(torch.device("cuda", device), non_blocking=True)
-    torch.cuda.synchronize(device)
-    del host
+    tdt = F.torch_dtype(store_dt)
+    dev = torch.device("cuda", device)
+    x = torch.empty(tuple(shape), dtype=tdt, device=dev)
+    spans = _row_spans(start[0], shape[0], int(info.chunk_shape[0])) if shape[0] > 0 else []
+    if spans and all(v > 0 for v in shape):
+        plane = int(np.prod(shape[1:])) if nd > 1 else 1
+        rows = max(b - a for a, b in spans)
+        nbuf = min(3, len(spans))
+        bufs = [torch.empty((rows * plane,), dtype=tdt, pin_memory=True) for _ in range(nbuf)]
+        evs = [None] * nbuf
+        stream = torch.cuda.Stream(device=dev)
+
+        def decode(k):
+            a, b = spans[k]
+            h = bufs[k % nbuf][:(b - a) * plane].view([b - a] + shape[1:])
+            S.read_array(path, [a] + start[1:], [b - a] + shape[1:], nthreads=nthreads,
+                         out=h.numpy())
+            return h
+
+        with ThreadPoolExecutor(1) as ex:
+            fut = ex.submit(decode, 0)
+            for k, (a, b) in enumerate(spans):
+                h = fut.result()
+                if k + 1 < len(spans):
+                    ev = evs[(k + 1) % nbuf]
+                    if ev is not None:
+                        ev.synchronize()  # the H2D that last read this buffer has finished
+                    fut = ex.submit(decode, k + 1)
+                with torch.cuda.stream(stream):
+                    x[a - start[0]:b - start[0]].copy_(h, non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record(stream)
+                evs[k % nbuf] = ev
+        stream.synchronize()
     return x.view(torch.bfloat16) if info.data_type == "bfloat16" else x
 
 
-def write_from_device(path, x, nthreads: int = 0) -> None:
-    """A device tensor (the whole array at `path`) through pinned host memory into the store."""
+def write_from_device(path, x, nthreads: int = 0, start=None) -> None:
+    """A device tensor (the box at `start`, default the whole array at `path`) into the store,
+    overlapped chunk row by chunk row: row k+1 is copied device-to-host into one of two pinned
+    buffers while a host thread encodes row k."""
     import torch
+    from concurrent.futures import ThreadPoolExecutor
     if x.dtype == torch.bfloat16:
         x = x.view(torch.uint16)
-    host = torch.empty(tuple(x.shape), dtype=x.dtype, pin_memory=True)
-    host.copy_(x)
-    S.write_array(path, host.numpy(), nthreads=nthreads)
+    info = S.open_array(path)
+    nd = x.dim()
+    start = [0] * nd if start is None else [int(v) for v in start]
+    shape = list(x.shape)
+    if not shape or any(v == 0 for v in shape):
+        return
+    spans = _row_spans(start[0], shape[0], int(info.chunk_shape[0]))
+    plane = int(np.prod(shape[1:])) if nd > 1 else 1
+    rows = max(b - a for a, b in spans)
+    nbuf = min(2, len(spans))
+    bufs = [torch.empty((rows * plane,), dtype=x.dtype, pin_memory=True) for _ in range(nbuf)]
+    futs = [None] * nbuf
+    with ThreadPoolExecutor(1) as ex:
+        for k, (a, b) in enumerate(spans):
+            if futs[k % nbuf] is not None:
+                futs[k % nbuf].result()  # this buffer's previous row is encoded
+            h = bufs[k % nbuf][:(b - a) * plane].view([b - a] + shape[1:])
+            h.copy_(x[a - start[0]:b - start[0]])
+            futs[k % nbuf] = ex.submit(S.write_array, path, h.numpy(), [a] + start[1:], nthreads)
+        for f in futs:
+            if f is not None:
+                f.result()
 
 
 def run_device_chain(steps: list, paths: list, device: int = 0, nthreads: int = 0,

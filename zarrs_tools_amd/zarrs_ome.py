@@ -170,6 +170,20 @@ def _reencode_level0(src, dst, encoding, nthreads, log, device: int = 0):
     log(f"0: reencode {src} -> {dst} ({out.data_type} {list(out.shape)})")
 
 
+def _ingest(path, device: int, nthreads: int, log):
+    """Level 0 into HBM (pipelined decode || H2D); (None, False) when an allocation is refused
+    (the store path then runs the levels)."""
+    t1 = time.perf_counter()
+    try:
+        x = read_to_device(path, device, nthreads)
+    except RuntimeError as e:
+        if not allocation_refused(e):
+            raise  # storage / codec errors are real failures
+        return None, False
+    log(f"   level 0 -> device in {time.perf_counter() - t1:.2f}s")
+    return x, True
+
+
 def _device_pyramid_fits(info, gauss, device: int, frac: float = 0.8, sharing: int = 1,
                          host_share: int = 1) -> bool:
     """Level 0 + the pyramid (< 1/7 of level 0 for 2x factors, bounded by level 0 here) + the
@@ -215,20 +229,24 @@ def _octant_worker(out_root: str, assign, factor, discrete: bool, device: int, n
     if compute is None:
         import torch
         from . import filter as F
-        store_dt = "uint16" if info0.data_type == "bfloat16" else info0.data_type
-        host = torch.empty(tuple(assign.shape), dtype=F.torch_dtype(store_dt), pin_memory=True)
-        S.read_array(lvl0, assign.start, assign.shape, nthreads=nthreads, out=host.numpy())
-        cur = host.to(torch.device("cuda", device), non_blocking=True)
-        torch.cuda.synchronize(device)
-        del host
-        if info0.data_type == "bfloat16":
-            cur = cur.view(torch.bfloat16)
+        # the box streamed into HBM chunk row by chunk row (decode || H2D)
+        cur = read_to_device(lvl0, device, nthreads, start=assign.start, shape=assign.shape)
+        st["read_s"] = time.perf_counter() - t0
+        t_pyr = time.perf_counter()
         ctx = F.default_context(device)
         ds = F.Downsample(factor, discrete=discrete)
+        # levels 1..L of the box in one call: up to three 2x2x2 mean levels per launch
+        # (zt_pyramid_downsample, the level-fused kernel), bit-identical to per-level launches
+        fused = F.pyramid(cur, factor, max_levels=assign.local_levels, discrete=discrete, ctx=ctx)
+        ctx.synchronize()
+        st["kernel_s"] = time.perf_counter() - t_pyr
+        fused_iter = iter(fused)
 
         def level(x):
-            y = ds._apply(x, None, discrete, ctx)
-            ctx.synchronize()
+            y = next(fused_iter, None)
+            if y is None:  # the box's own stop rule ended early: one level at a time
+                y = ds._apply(x, None, discrete, ctx)
+                ctx.synchronize()
             return y
 
         def to_host(x):
@@ -240,7 +258,7 @@ def _octant_worker(out_root: str, assign, factor, discrete: bool, device: int, n
     else:
         cur = S.read_array(lvl0, assign.start, assign.shape, nthreads=nthreads)
         level, to_host = compute, (lambda x: x)
-    st["read_s"] = time.perf_counter() - t0
+        st["read_s"] = time.perf_counter() - t0
     for k in range(1, assign.local_levels + 1):
         bstart, bshape = assign.level_boxes[k - 1]
         t1 = time.perf_counter()
@@ -383,13 +401,46 @@ def run(input_path, output_path, factor=None, max_levels: int = 10, discrete: bo
             shutil.rmtree(output_path)
     os.makedirs(output_path, exist_ok=True)
     lvl0 = os.path.join(output_path, "0")
+    # level shapes (downsample.rs:162-168) and the stop rule (:731-737): known from the input
+    level_shapes = []
+    cur_shape = list(info.shape)
+    for _ in range(max_levels):
+        cur_shape = [max(s // f, 1) for s, f in zip(cur_shape, factor)]
+        level_shapes.append(cur_shape)
+        if all(f == 1 or s == 1 for f, s in zip(factor, cur_shape)):
+            break
+    multi = gpus > 1 and _device_ok(device)
+    dt0 = (reencoding or {}).get("data_type") or info.data_type
+    info0 = S.ArrayInfo(lvl0, dt0, tuple(info.shape), info.chunk_shape, info.inner_chunk_shape)
+    on_device = (not multi and device_resident and _device_ok(device)
+                 and _device_pyramid_fits(info0, gauss, device))
+    cur = None  # the previous level in HBM (device-resident pyramid)
     if reencoding:
         _reencode_level0(input_path, lvl0, reencoding, nthreads, log, device)
     else:
         if os.path.exists(lvl0):
             shutil.rmtree(lvl0)
-        shutil.copytree(input_path, lvl0)
+        # level 0 is a copy of the input (copy_dir, zarrs_ome.rs:341-356); the device-resident
+        # pyramid streams the same input into HBM meanwhile (the copy's reads warm the page
+        # cache for it, or the other way round), so level 0 costs one pass over the input
+        import threading
+        copy_err = []
+
+        def _copy():
+            try:
+                shutil.copytree(input_path, lvl0)
+            except BaseException as e:  # re-raised below
+                copy_err.append(e)
+        th = threading.Thread(target=_copy)
+        th.start()
+        if on_device:
+            cur, on_device = _ingest(input_path, device, nthreads, log)
+        th.join()
+        if copy_err:
+            raise copy_err[0]
         log(f"0: copy {input_path} -> {lvl0} ({info.data_type} {list(info.shape)})")
+    if on_device and cur is None:
+        cur, on_device = _ingest(lvl0, device, nthreads, log)
     # move array 0's attributes to the group (zarrs_ome.rs:368-377)
     meta0_path = os.path.join(lvl0, "zarr.json")
     with open(meta0_path) as f:
@@ -408,14 +459,6 @@ def run(input_path, output_path, factor=None, max_levels: int = 10, discrete: bo
     shape = list(S.open_array(lvl0).shape)
     stats = []
     lvl0_info = S.open_array(lvl0)
-    level_shapes = []
-    cur_shape = list(shape)
-    for _ in range(max_levels):  # downsample.rs:162-168 + the stop rule (:731-737)
-        cur_shape = [max(s // f, 1) for s, f in zip(cur_shape, factor)]
-        level_shapes.append(cur_shape)
-        if all(f == 1 or s == 1 for f, s in zip(factor, cur_shape)):
-            break
-    multi = gpus > 1 and _device_ok(device)
     octants_done = 0  # levels 1..octants_done computed by run_octants
     if multi and gauss is None and level_shapes:
         from . import shard
@@ -433,20 +476,19 @@ def run(input_path, output_path, factor=None, max_levels: int = 10, discrete: bo
                                                discrete, gpus, devices, nthreads, log)
             st_oct["levels"] = octants_done
             stats.append(st_oct)
-    on_device = (not multi and device_resident and _device_ok(device)
-                 and _device_pyramid_fits(lvl0_info, gauss, device))
-    cur = None  # the previous level in HBM (device-resident pyramid)
+    fused_levels = None  # every level of the device-resident mean / mode pyramid, one call
     if on_device:
         from . import filter as F
         ctx = F.default_context(device)
-        t1 = time.perf_counter()
-        try:
-            cur = read_to_device(lvl0, device, nthreads)
-        except RuntimeError as e:
-            if not allocation_refused(e):
-                raise  # storage / codec errors are real failures
-            on_device = False  # pinned host or device allocation refused: the store path
-        log(f"   level 0 -> device in {time.perf_counter() - t1:.2f}s")
+        if gauss is None:
+            # zt_pyramid_downsample: up to three 2x2x2 mean levels per launch (level-fused
+            # kernel), bit-identical to the per-level launches
+            t1 = time.perf_counter()
+            fused_levels = F.pyramid(cur, factor, max_levels=len(level_shapes), discrete=discrete,
+                                     ctx=ctx)
+            ctx.synchronize()
+            t_pyr = time.perf_counter() - t1
+            log(f"   levels 1-{len(fused_levels)} on the device in {t_pyr:.3f}s")
     for i in range(1, len(level_shapes) + 1):
         src, dst = os.path.join(output_path, str(i - 1)), os.path.join(output_path, str(i))
         src_info = S.open_array(src)
@@ -460,14 +502,20 @@ def run(input_path, output_path, factor=None, max_levels: int = 10, discrete: bo
             t1 = time.perf_counter()
             S.create_output(src, dst, None, out_shape, enc)
             _hold_metadata(dst)
-            v = cur
-            if gauss is not None:
-                v = F.Gaussian(gauss[0], gauss[1]).apply_ndarray(v, dtype_out="float32", ctx=ctx)
-            ds = F.Downsample(factor, discrete=discrete)
-            nxt = ds._apply(v, src_info.data_type, discrete, ctx)
-            nxt = nxt.reshape(out_shape)
-            ctx.synchronize()
-            t_k = time.perf_counter() - t1
+            if fused_levels is not None and i <= len(fused_levels):
+                nxt = fused_levels[i - 1]
+                fused_levels[i - 1] = None
+                t_k = t_pyr if i == 1 else 0.0
+            else:
+                v = cur
+                if gauss is not None:
+                    v = F.Gaussian(gauss[0], gauss[1]).apply_ndarray(v, dtype_out="float32",
+                                                                     ctx=ctx)
+                ds = F.Downsample(factor, discrete=discrete)
+                nxt = ds._apply(v, src_info.data_type, discrete, ctx)
+                nxt = nxt.reshape(out_shape)
+                ctx.synchronize()
+                t_k = time.perf_counter() - t1
             t2 = time.perf_counter()
             write_from_device(dst, nxt, nthreads)
             _publish_metadata(dst)
