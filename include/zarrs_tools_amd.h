@@ -330,6 +330,14 @@ int zt_store_guided_filter(const char* in_path, const char* out_path, int dtype_
                            const char* encoding_json, float epsilon, int radius, int device,
                            int64_t row_begin, int64_t row_end, int nthreads, int flags,
                            zt_store_stats* stats);
+/* zt_store_guided_filter restricted to the output chunk columns [col_begin, col_end) along
+ * axis 1 (col_end < 0: all), the input read with the 2r halo along axes 0 and 1: one process's
+ * (t, z) block of a multi-GPU split (config T; the reference's per-chunk loop,
+ * guided_filter.rs:260-316, over that block's chunks). */
+int zt_store_guided_filter_box(const char* in_path, const char* out_path, int dtype_out,
+                               const char* encoding_json, float epsilon, int radius, int device,
+                               int64_t row_begin, int64_t row_end, int64_t col_begin,
+                               int64_t col_end, int nthreads, int flags, zt_store_stats* stats);
 /* zarrs_filter downsample / one zarrs_ome level over a store (Downsample::apply,
  * downsample.rs:170-286): output shape max(n / stride, 1), encoding as the input's with the
  * encoding_json overrides (zarrs_ome passes its per-level chunk / shard shapes). */

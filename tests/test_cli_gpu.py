@@ -401,3 +401,30 @@ def test_chunk_limit_bounds_chunks_in_flight(tmp_path):
     a = S.read_array(tmp_path / "a.zarr")
     assert np.array_equal(a, S.read_array(tmp_path / "b.zarr"))
     assert np.array_equal(a, S.read_array(tmp_path / "c.zarr"))
+
+
+@pytest.mark.parametrize("groups", [(2, 2), (1, 3), (3, 1)])
+def test_store_guided_filter_tz_blocks_equal_whole(tmp_path, groups):
+    """zt_store_guided_filter_box: the output written block by block — (t, z) boxes of whole
+    chunks (shard.block_assignment), each read with the 2r halo along t and z — equals the
+    one-call store output bit for bit, and the oracle within the float tolerance."""
+    from zarrs_tools_amd import shard
+    shape, chunk = (10, 22, 12, 20), (4, 8, 12, 10)
+    v = O.synth_step_noise_f32(shape)
+    S.create_array(tmp_path / "in.zarr", "float32", shape, chunk)
+    S.write_array(tmp_path / "in.zarr", v)
+    S.guided_filter(tmp_path / "in.zarr", tmp_path / "whole.zarr", 2500.0, 2)
+    S.create_output(tmp_path / "in.zarr", tmp_path / "blocks.zarr", None, shape, None)
+    world = groups[0] * groups[1]
+    nt, nz = -(-shape[0] // chunk[0]), -(-shape[1] // chunk[1])
+    for r in range(world):
+        a = shard.block_assignment(r, world, shape, chunk, 4, groups)
+        rows = (a.out_start[0] // chunk[0], -(-(a.out_start[0] + a.out_shape[0]) // chunk[0]))
+        cols = (a.out_start[1] // chunk[1], -(-(a.out_start[1] + a.out_shape[1]) // chunk[1]))
+        assert rows[1] <= nt and cols[1] <= nz
+        S.guided_filter(tmp_path / "in.zarr", tmp_path / "blocks.zarr", 2500.0, 2, rows=rows,
+                        cols=cols, erase=False, finish=False)
+    got = S.read_array(tmp_path / "blocks.zarr")
+    assert np.array_equal(got, S.read_array(tmp_path / "whole.zarr"))
+    want = O.guided_filter_apply(v, chunk, 2500.0, 2, nthreads=8)
+    assert rel_err(got, want) <= FLOAT_TOL

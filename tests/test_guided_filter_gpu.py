@@ -299,6 +299,42 @@ def test_guided4d_per_chunk_and_small_eps(r):
     assert rel_err(gpu_apply_chunked(v, "float32", "float32", chunk, 0.5, r), ref) <= FLOAT_TOL
 
 
+@pytest.mark.parametrize("shape,chunk,r", [
+    ((20, 9, 14, 40), (4, 4, 8, 16), 2),     # a (t, z) block of config T: 16 + 2r timepoints
+    ((32, 6, 7, 20), (8, 3, 7, 10), 3),      # TMAX = 32
+    ((17, 10, 12, 33), (5, 5, 6, 11), 6),
+    ((12, 8, 9, 30), (4, 4, 9, 15), 1),      # TMAX = 16
+])
+def test_guided4d_long_series_small_eps(shape, chunk, r):
+    """The four-kernel 4-D path for blocks of 5-32 timepoints (sliding t-windows, stage 2 as box3
+    of the t-window sums with the final stage in the box3 march): whole box and per chunk equal
+    the oracle at eps = 0.5 (exact stage 1)."""
+    rng = np.random.default_rng(sum(shape) + r)
+    v = (rng.random(shape, dtype=np.float32) * 300).astype(np.float32)
+    ref = O.guided_filter_apply(v, chunk, 0.5, r, nthreads=8)
+    assert rel_err(gpu_apply(v, "float32", "float32", chunk, 0.5, r), ref) <= FLOAT_TOL
+    assert rel_err(gpu_apply_chunked(v, "float32", "float32", chunk, 0.5, r), ref) <= FLOAT_TOL
+
+
+def test_guided4d_block_output_box_vs_oracle():
+    """apply_ndarray on a halo'd (t, z) block with an interior output box (the config T share
+    form, tools/bench_ops.py): equals the oracle's per-chunk result of the whole array."""
+    from zarrs_tools_amd import shard
+    import torch
+    shape, chunk, r = (16, 20, 12, 40), (4, 5, 12, 40), 2
+    rng = np.random.default_rng(3)
+    v = (rng.random(shape, dtype=np.float32) * 300).astype(np.float32)
+    ref = O.guided_filter_apply(v, chunk, 0.5, r, nthreads=8)
+    for rank in range(4):
+        a = shard.block_assignment(rank, 4, shape, chunk, 2 * r, (2, 2))
+        blk = np.ascontiguousarray(v[tuple(slice(s, s + n) for s, n in zip(a.in_start, a.in_shape))])
+        x = torch.from_numpy(blk).cuda()
+        sub = zt.ArraySubset(tuple(o - i for o, i in zip(a.out_start, a.in_start)), a.out_shape)
+        got = zt.GuidedFilter(0.5, r).apply_ndarray(x, sub).cpu().numpy()
+        want = ref[tuple(slice(o, o + n) for o, n in zip(a.out_start, a.out_shape))]
+        assert rel_err(got, want) <= FLOAT_TOL, rank
+
+
 # ---- 4-D one-march kernel (g4_fused.hip): T <= 4 timepoints per block, r <= 2 ---------------
 
 @pytest.mark.parametrize("shape,chunk,r", [

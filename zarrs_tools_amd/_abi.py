@@ -183,6 +183,10 @@ def lib() -> ctypes.CDLL:
         "zt_store_guided_filter": ([ctypes.c_char_p, ctypes.c_char_p, c_int, ctypes.c_char_p,
                                     c_float, c_int, c_int, ctypes.c_int64, ctypes.c_int64, c_int,
                                     c_int, ctypes.POINTER(StoreStats)], c_int),
+        "zt_store_guided_filter_box": ([ctypes.c_char_p, ctypes.c_char_p, c_int, ctypes.c_char_p,
+                                        c_float, c_int, c_int, ctypes.c_int64, ctypes.c_int64,
+                                        ctypes.c_int64, ctypes.c_int64, c_int, c_int,
+                                        ctypes.POINTER(StoreStats)], c_int),
         "zt_store_downsample": ([ctypes.c_char_p, ctypes.c_char_p, i64p, c_int, c_int,
                                  ctypes.c_char_p, c_int, ctypes.c_int64, ctypes.c_int64, c_int,
                                  c_int, ctypes.POINTER(StoreStats)], c_int),

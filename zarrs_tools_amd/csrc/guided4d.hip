@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 #include "zt_device.hpp"
@@ -346,6 +347,196 @@ __global__ __launch_bounds__(256) void g4_final_slide_kernel(const float2* __res
     }
 }
 
+// ---- three-kernel form (round 4): stage 2 as box3 of the t-window sums ------------------------
+// box4(a, b) = box3(tbox(a, b)) (the sums are separable; stage 2 is rounded to f32 anyway), so
+//   K2t: per voxel, all T timepoints in registers: U4 = t-window of U3 (exact), u, a, b, and
+//        TAB(t) = t-window sums of (a, b) (f64, rounded to f32 once) for the OUTPUT timepoints
+//        only, written over U3's storage (a thread reads every U3 of its voxel first);
+//   K3f: box3 z-march of TAB over the output box with the final stage fused into its output:
+//        mean = (f32)S4 / c4, out = RN(RN(v * ma) + mb) (guided_filter.rs:144-163), stored as TOut.
+// Against K2 / K3 / K4 this drops the AB and S3 round trips and K3's halo timepoints: about
+// 12 + 12 + 16 B per voxel instead of ~64.
+template <int TMAX, int R>
+__global__ __launch_bounds__(256) void g4_tab_kernel(double* __restrict__ U3T,
+                                                     const float* __restrict__ v, int T, int t0,
+                                                     int ont, int nz, int ny, int nx, float eps,
+                                                     Str3 vs) {
+    const int64_t vol = (int64_t)nz * ny * nx;
+    const int x = blockIdx.x * kPX + threadIdx.x, y = blockIdx.y * kPY + threadIdx.y;
+    if (x >= nx || y >= ny) return;
+    const int cyx = ccount(y, ny, R) * ccount(x, nx, R);
+    float2* TAB = reinterpret_cast<float2*>(U3T);
+    const int tlo = t0 - R, thi = t0 + ont + R;  // (a, b) needed on [tlo, thi)
+    for (int z = blockIdx.z; z < nz; z += gridDim.z) {
+        const int64_t i = ((int64_t)z * ny + y) * nx + x;
+        const int c3 = ccount(z, nz, R) * cyx;
+        double U[TMAX];
+#pragma unroll
+        for (int t = 0; t < TMAX; ++t) U[t] = t < T ? U3T[t * vol + i] : 0.0;
+        float2 ab[TMAX];
+        double W = 0.0;  // t-window of U3 for timepoint t (values past T are 0)
+#pragma unroll
+        for (int j = 0; j < R && j < TMAX; ++j) W += U[j];
+#pragma unroll
+        for (int t = 0; t < TMAX + R; ++t) {
+            if (t < TMAX) {
+                if (t + R < TMAX) W += U[t + R];
+                if (t - R - 1 >= 0) W -= U[t - R - 1];
+                ab[t] = make_float2(0.f, 0.f);
+                if (t < T && t >= tlo && t < thi) {
+                    const int ta = max(t - R, 0), tb = min(t + R, T - 1);
+                    const float cnt = (float)(c3 * (tb - ta + 1));
+                    const float u = (float)W / cnt;  // summed_area_table_mean
+                    const float d = v[t * vs.t + (int64_t)z * vs.z + (int64_t)y * vs.y + x] - u;
+                    const float sq = d * d;  // (v - u).powf(2.0)
+                    const float a = sq / (sq + eps);
+                    ab[t] = make_float2(a, (1.0f - a) * u);
+                }
+            }
+            const int tt = t - R;  // every (a, b) of its window is known now
+            if (tt >= 0 && tt < TMAX && tt < T && tt >= t0 && tt < t0 + ont) {
+                double sa = 0.0, sb = 0.0;
+#pragma unroll
+                for (int j = -R; j <= R; ++j)
+                    if (tt + j >= 0 && tt + j < TMAX) {
+                        sa += (double)ab[tt + j].x;
+                        sb += (double)ab[tt + j].y;
+                    }
+                TAB[(int64_t)(tt - t0) * vol + i] = make_float2((float)sa, (float)sb);
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ void store_dtype(void* out, int dtype, int64_t i, float o) {
+    switch (dtype) {
+    case kBool: case kU8: static_cast<uint8_t*>(out)[i] = from_f32<uint8_t>(o); break;
+    case kI8: static_cast<int8_t*>(out)[i] = from_f32<int8_t>(o); break;
+    case kI16: static_cast<int16_t*>(out)[i] = from_f32<int16_t>(o); break;
+    case kI32: static_cast<int32_t*>(out)[i] = from_f32<int32_t>(o); break;
+    case kI64: static_cast<int64_t*>(out)[i] = from_f32<int64_t>(o); break;
+    case kU16: static_cast<uint16_t*>(out)[i] = from_f32<uint16_t>(o); break;
+    case kU32: static_cast<uint32_t*>(out)[i] = from_f32<uint32_t>(o); break;
+    case kU64: static_cast<uint64_t*>(out)[i] = from_f32<uint64_t>(o); break;
+    case kBF16: static_cast<bf16_t*>(out)[i] = from_f32<bf16_t>(o); break;
+    case kF16: static_cast<f16_t*>(out)[i] = from_f32<f16_t>(o); break;
+    case kF64: static_cast<double*>(out)[i] = from_f32<double>(o); break;
+    default: static_cast<float*>(out)[i] = o; break;
+    }
+}
+
+// K3f: one workgroup marches one 64 x kTY xy tile of the OUTPUT box through a z segment of it, for
+// one output timepoint; the running z-window (f64 pair) covers the tile's R apron, whose loads
+// reach into the block's halo (zero outside the block: the clamped windows).
+template <int R>
+__global__ __launch_bounds__(kNT) void box3_final_kernel(const float2* __restrict__ TAB,
+                                                         const float* __restrict__ v,
+                                                         void* __restrict__ out, int dtype_out,
+                                                         NdGeom g, int zseg, int tiles_x,
+                                                         int tiles_y, Str3 vs) {
+    constexpr int EX = kTX + 2 * R, EY = kTY + 2 * R, NE = EX * EY;
+    constexpr int NPT = (NE + kNT - 1) / kNT;
+    __shared__ dd2 Z[EY][EX];
+    __shared__ dd2 X[EY][kTX];
+    const int T = (int)g.shape[0], nz = (int)g.shape[1], ny = (int)g.shape[2],
+              nx = (int)g.shape[3];
+    const int ot = blockIdx.y;
+    const int t = ot + (int)g.out_start[0];
+    const int ntile = tiles_x * tiles_y;
+    const int seg = blockIdx.x / ntile, tile = blockIdx.x % ntile;
+    const int ox0 = (int)g.out_start[3], oy0 = (int)g.out_start[2], oz0 = (int)g.out_start[1];
+    const int ox1 = ox0 + (int)g.out_shape[3], oy1 = oy0 + (int)g.out_shape[2];
+    const int x0 = ox0 + (tile % tiles_x) * kTX, y0 = oy0 + (tile / tiles_x) * kTY;
+    const int z0 = oz0 + seg * zseg, z1 = min(z0 + zseg, oz0 + (int)g.out_shape[1]);
+    const int64_t plane = (int64_t)ny * nx;
+    const float2* vol = TAB + (int64_t)ot * nz * plane;
+    const int ct = min(t + R, T - 1) - max(t - R, 0) + 1;
+
+    int64_t pidx[NPT];
+    int ey_[NPT], ex_[NPT];
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+        const int e = threadIdx.x + k * kNT;
+        const int ey = e / EX, ex = e % EX;
+        const int gy = y0 - R + ey, gx = x0 - R + ex;
+        ey_[k] = e < NE ? ey : -1;
+        ex_[k] = ex;
+        pidx[k] = (e < NE && gy >= 0 && gy < ny && gx >= 0 && gx < nx) ? (int64_t)gy * nx + gx : -1;
+    }
+    auto load = [&](int z, int k) -> float2 {
+        return (pidx[k] >= 0 && z >= 0 && z < nz) ? vol[(int64_t)z * plane + pidx[k]]
+                                                   : make_float2(0.f, 0.f);
+    };
+    dd2 zs[NPT];
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {  // window of slice z0 - 1
+        acc_zero(zs[k]);
+        for (int z = z0 - 1 - R; z <= z0 - 1 + R; ++z) acc_add(zs[k], load(z, k));
+    }
+    float2 pa[NPT], ps[NPT];
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+        pa[k] = load(z0 + R, k);
+        ps[k] = load(z0 - R - 1, k);
+    }
+    for (int z = z0; z < z1; ++z) {
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) {
+            acc_add(zs[k], pa[k]);
+            acc_sub(zs[k], ps[k]);
+            if (ey_[k] >= 0) Z[ey_[k]][ex_[k]] = zs[k];
+        }
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) {
+            pa[k] = load(z + 1 + R, k);
+            ps[k] = load(z - R, k);
+        }
+        __syncthreads();
+        for (int it = threadIdx.x; it < EY * (kTX / kKX); it += kNT) {
+            const int ey = it / (kTX / kKX), sx = (it % (kTX / kKX)) * kKX;
+            dd2 sacc;
+            acc_zero(sacc);
+#pragma unroll
+            for (int j = 0; j <= 2 * R; ++j) acc_add(sacc, Z[ey][sx + j]);
+            X[ey][sx] = sacc;
+#pragma unroll
+            for (int j = 1; j < kKX; ++j) {
+                acc_add(sacc, Z[ey][sx + j + 2 * R]);
+                acc_sub(sacc, Z[ey][sx + j - 1]);
+                X[ey][sx + j] = sacc;
+            }
+        }
+        __syncthreads();
+        {
+            const int tx = threadIdx.x % kTX, sy = (threadIdx.x / kTX) * kKY;
+            const int gx = x0 + tx;
+            const int czx = ccount(z, nz, R) * ccount(gx, nx, R) * ct;
+            dd2 sacc;
+            acc_zero(sacc);
+#pragma unroll
+            for (int j = 0; j <= 2 * R; ++j) acc_add(sacc, X[sy + j][tx]);
+#pragma unroll
+            for (int j = 0; j < kKY; ++j) {
+                if (j > 0) {
+                    acc_add(sacc, X[sy + j + 2 * R][tx]);
+                    acc_sub(sacc, X[sy + j - 1][tx]);
+                }
+                const int gy = y0 + sy + j;
+                if (gx < ox1 && gy < oy1) {
+                    const float cnt = (float)(czx * ccount(gy, ny, R));
+                    const float ma = (float)sacc.x / cnt, mb = (float)sacc.y / cnt;
+                    const float vv = v[t * vs.t + (int64_t)z * vs.z + (int64_t)gy * vs.y + gx];
+                    const float o = __fadd_rn(__fmul_rn(vv, ma), mb);  // v *= ma; v += mb
+                    store_dtype(out, dtype_out,
+                                ot * g.out_strides[0] + (z - oz0) * g.out_strides[1] +
+                                    (gy - oy0) * g.out_strides[2] + (gx - ox0) * g.out_strides[3],
+                                o);
+                }
+            }
+        }
+    }
+}
+
 template <int R, typename TV, typename TA, typename TO>
 hipError_t launch_box3(const TV* in, TO* out, int T, int nz, int ny, int nx, Str3 is,
                        hipStream_t s) {
@@ -382,9 +573,19 @@ hipError_t launch_box3_r(int r, const TV* in, TO* out, int T, int nz, int ny, in
 // checked by the caller (K2 / K4 hold a voxel's timepoints in registers, y is grid.y)
 bool guided4d_supports(int radius) { return radius >= 1 && radius <= 6; }
 
+// ZT_G4_LEGACY=1: the four-kernel form (K2 / K3 / K4 with the AB and S3 round trips; A/B runs)
+static bool g4_legacy() {
+    static const bool on = [] {
+        const char* e = getenv("ZT_G4_LEGACY");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+
 int64_t guided4d_scratch_bytes(int64_t numel, bool gather) {
-    // U3 / S3 (8 B) | AB (8 B) | v (4 B, when the input is not a contiguous f32 block)
-    return numel * (16 + (gather ? 4 : 0)) + 64;
+    // U3 / S3 / TAB (8 B) | AB (8 B, four-kernel form only) | v (4 B, when the input is not a
+    // contiguous f32 block)
+    return numel * ((g4_legacy() ? 16 : 8) + (gather ? 4 : 0)) + 64;
 }
 
 hipError_t launch_guided4d(const void* in, int dtype_in, void* out, int dtype_out,
@@ -417,6 +618,58 @@ hipError_t launch_guided4d(const void* in, int dtype_in, void* out, int dtype_ou
     e = launch_box3_r<float, double, double>(radius, v, U3, T, nz, ny, nx, vs, s);
     if (e != hipSuccess) return e;
     if (ny > 65535 || g.out_shape[2] > 65535) return hipErrorInvalidValue;  // grid.y
+    if (!g4_legacy()) {
+        // three-kernel form: K2t (u, a, b and their t-window sums for the output timepoints)
+        // then the box3 march of those with the final stage in its output (K3f)
+        const int t0 = (int)g.out_start[0], ont = (int)g.out_shape[0];
+        const int64_t pgx = (nx + kPX - 1) / kPX, pgy = (ny + kPY - 1) / kPY;
+        const dim3 pgrid((unsigned)pgx, (unsigned)pgy,
+                         (unsigned)std::min<int64_t>(nz, std::max<int64_t>(1, 65536 / (pgy * pgx) + 1)));
+        const dim3 pblock(kPX, kPY);
+        auto k2t = [&](auto tm, auto rr) {
+            constexpr int TM = decltype(tm)::value, RR = decltype(rr)::value;
+            hipLaunchKernelGGL((g4_tab_kernel<TM, RR>), pgrid, pblock, 0, s, U3, v, T, t0, ont, nz,
+                               ny, nx, eps, vs);
+        };
+        auto k2r = [&](auto tm) {
+            switch (radius) {
+            case 1: k2t(tm, std::integral_constant<int, 1>{}); break;
+            case 2: k2t(tm, std::integral_constant<int, 2>{}); break;
+            case 3: k2t(tm, std::integral_constant<int, 3>{}); break;
+            case 4: k2t(tm, std::integral_constant<int, 4>{}); break;
+            case 5: k2t(tm, std::integral_constant<int, 5>{}); break;
+            case 6: k2t(tm, std::integral_constant<int, 6>{}); break;
+            default: break;
+            }
+        };
+        if (T <= 4) k2r(std::integral_constant<int, 4>{});
+        else if (T <= 16) k2r(std::integral_constant<int, 16>{});
+        else if (T <= 32) k2r(std::integral_constant<int, 32>{});
+        else return hipErrorInvalidValue;
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        const int64_t onx = g.out_shape[3], ony = g.out_shape[2], onz = g.out_shape[1];
+        const int tiles_x = (int)((onx + kTX - 1) / kTX), tiles_y = (int)((ony + kTY - 1) / kTY);
+        const int64_t tiles = (int64_t)tiles_x * tiles_y;
+        int nseg = (int)std::max<int64_t>(
+            1, std::min<int64_t>((onz + 15) / 16, (4096 + tiles * ont - 1) / (tiles * ont)));
+        const int zseg = (int)((onz + nseg - 1) / nseg);
+        nseg = (int)((onz + zseg - 1) / zseg);
+        const int64_t gx = tiles * nseg;
+        if (gx > 0x7FFFFFFF || ont > 65535) return hipErrorInvalidValue;
+        const float2* TAB = reinterpret_cast<const float2*>(U3);
+        const dim3 fg((unsigned)gx, (unsigned)ont);
+        switch (radius) {
+#define ZT_G4_K3F(RR)                                                                             \
+    case RR:                                                                                      \
+        hipLaunchKernelGGL((box3_final_kernel<RR>), fg, dim3(kNT), 0, s, TAB, v, out, dtype_out,   \
+                           g, zseg, tiles_x, tiles_y, vs);                                        \
+        break;
+            ZT_G4_K3F(1) ZT_G4_K3F(2) ZT_G4_K3F(3) ZT_G4_K3F(4) ZT_G4_K3F(5) ZT_G4_K3F(6)
+#undef ZT_G4_K3F
+        default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
     // (a, b) are needed only within R timepoints of the output's (a slab's halo timepoints
     // beyond that feed stage 1 alone)
     const int ta_ab = std::max<int>(0, (int)g.out_start[0] - radius);

@@ -146,7 +146,9 @@ std::vector<int64_t> c_strides(const std::vector<int64_t>& shape) {
 }
 
 // every chunk index of the chunk rows [r0, r1) along axis 0
-std::vector<std::vector<int64_t>> chunks_in_rows(const Array& a, int64_t r0, int64_t r1) {
+// Chunks of rows [r0, r1) along axis 0 whose axis-1 index lies in [c0, c1) (c1 < 0: all).
+std::vector<std::vector<int64_t>> chunks_in_rows(const Array& a, int64_t r0, int64_t r1,
+                                                 int64_t c0 = 0, int64_t c1 = -1) {
     const auto g = a.grid_shape();
     const int nd = a.ndim();
     int64_t per = 1;
@@ -158,10 +160,17 @@ std::vector<std::vector<int64_t>> chunks_in_rows(const Array& a, int64_t r0, int
             idx[0] = r;
             int64_t rem = c;
             for (int d = nd - 1; d >= 1; --d) { idx[d] = rem % g[d]; rem /= g[d]; }
+            if (nd > 1 && c1 >= 0 && (idx[1] < c0 || idx[1] >= c1)) continue;
             out.push_back(idx);
         }
     return out;
 }
+
+// An output window along axis 1 (config T's (t, z) block split): output elements [o0, o1) and
+// the input elements [i0, i1) they read (the halo, clamped). Absent: the whole axis.
+struct ColWin {
+    int64_t o0, o1, i0, i1;
+};
 
 struct Pinned {
     void* p = nullptr;
@@ -576,7 +585,8 @@ struct RowOp {
 };
 
 void run_pipeline(const Array& in, const Array& out, int device, int64_t row_begin,
-                  int64_t row_end, int nthreads, const RowOp& op, zt_store_stats* st) {
+                  int64_t row_end, int nthreads, const RowOp& op, zt_store_stats* st,
+                  const ColWin* cw = nullptr) {
     const auto t_start = Clock::now();
     const int nd = in.ndim();
     const int64_t in_cz = in.chunk_shape[0], out_cz = out.chunk_shape[0];
@@ -586,8 +596,13 @@ void run_pipeline(const Array& in, const Array& out, int device, int64_t row_beg
     row_end = row_end < 0 ? out_rows : std::min(row_end, out_rows);
     if (row_begin >= row_end) return;
     int64_t in_plane = 1, out_plane = 1;
-    for (int d = 1; d < nd; ++d) in_plane *= in.shape[d];
-    for (int d = 1; d < out.ndim(); ++d) out_plane *= out.shape[d];
+    for (int d = 1; d < nd; ++d) in_plane *= (cw && d == 1) ? cw->i1 - cw->i0 : in.shape[d];
+    for (int d = 1; d < out.ndim(); ++d) out_plane *= (cw && d == 1) ? cw->o1 - cw->o0 : out.shape[d];
+    // chunk index ranges of the window along axis 1
+    const int64_t ic0 = cw ? cw->i0 / in.chunk_shape[1] : 0;
+    const int64_t ic1 = cw ? (cw->i1 + in.chunk_shape[1] - 1) / in.chunk_shape[1] : -1;
+    const int64_t oc0 = cw ? cw->o0 / out.chunk_shape[1] : 0;
+    const int64_t oc1 = cw ? (cw->o1 + out.chunk_shape[1] - 1) / out.chunk_shape[1] : -1;
     const size_t in_pb = (size_t)in_plane * in.esz, out_pb = (size_t)out_plane * out.esz;
 
     // input row span of each output row, and the largest slab
@@ -617,8 +632,8 @@ void run_pipeline(const Array& in, const Array& out, int device, int64_t row_beg
     // --chunk-limit: the chunks held in flight (decoded input rows + output rows being computed
     // or encoded) stay within the limit, down to the pipeline's unit of one slab and one output
     // row without overlap (a chunk row is the device's unit of work)
-    const int64_t in_row_chunks = (int64_t)chunks_in_rows(in, 0, 1).size();
-    const int64_t out_row_chunks = (int64_t)chunks_in_rows(out, 0, 1).size();
+    const int64_t in_row_chunks = (int64_t)chunks_in_rows(in, 0, 1, ic0, ic1).size();
+    const int64_t out_row_chunks = (int64_t)chunks_in_rows(out, 0, 1, oc0, oc1).size();
     int threads = resolve_threads(nthreads);
     if (g_chunk_limit > 0) {
         while (NR * in_row_chunks + NB * out_row_chunks > g_chunk_limit) {
@@ -673,14 +688,17 @@ void run_pipeline(const Array& in, const Array& out, int device, int64_t row_beg
     std::atomic<int64_t> dec_ns{0}, enc_ns{0}, k_us{0}, chunks_done{0};
     double h2d_ms = 0, k_ms = 0, d2h_ms = 0;
     int64_t chunks_total = 0;
-    for (int64_t k = row_begin; k < row_end; ++k) chunks_total += (int64_t)chunks_in_rows(out, k, k + 1).size();
+    for (int64_t k = row_begin; k < row_end; ++k)
+        chunks_total += (int64_t)chunks_in_rows(out, k, k + 1, oc0, oc1).size();
 
-    // region descriptors of a host row buffer (C order, in_cz planes)
+    // region descriptors of a host row buffer (C order, in_cz planes; the axis-1 window)
     std::vector<int64_t> in_row_shape(in.shape);
     in_row_shape[0] = in_cz;
+    if (cw) in_row_shape[1] = cw->i1 - cw->i0;
     const std::vector<int64_t> in_row_st = c_strides(in_row_shape);
     std::vector<int64_t> out_row_shape(out.shape);
     out_row_shape[0] = out_cz;
+    if (cw) out_row_shape[1] = cw->o1 - cw->o0;
     const std::vector<int64_t> out_row_st = c_strides(out_row_shape);
 
     auto submit_decode = [&](int64_t j) {
@@ -691,11 +709,12 @@ void run_pipeline(const Array& in, const Array& out, int device, int64_t row_beg
         }
         ring_row[s] = j;
         uint8_t* buf = hin[s].u8();
-        for (auto& idx : chunks_in_rows(in, j, j + 1)) {
+        for (auto& idx : chunks_in_rows(in, j, j + 1, ic0, ic1)) {
             pool.submit(dec_group[s], [&, idx, buf, j] {
                 const auto t0 = Clock::now();
                 std::vector<int64_t> origin(nd, 0);
                 origin[0] = j * in_cz;
+                if (cw) origin[1] = cw->i0;
                 size_t n = in.read_chunk(idx.data(), buf, origin.data(), in_row_shape.data(),
                                          in_row_st.data());
                 bytes_read += n;
@@ -706,11 +725,12 @@ void run_pipeline(const Array& in, const Array& out, int device, int64_t row_beg
     auto submit_encode = [&](int64_t k) {
         const int s = (int)(k % NB);
         uint8_t* buf = hout[s].u8();
-        for (auto& idx : chunks_in_rows(out, k, k + 1)) {
+        for (auto& idx : chunks_in_rows(out, k, k + 1, oc0, oc1)) {
             pool.submit(enc_group[s], [&, idx, buf, k] {
                 const auto t0 = Clock::now();
                 std::vector<int64_t> origin(out.ndim(), 0);
                 origin[0] = k * out_cz;
+                if (cw) origin[1] = cw->o0;
                 size_t n = out.write_chunk(idx.data(), buf, origin.data(), out_row_shape.data(),
                                            out_row_st.data());
                 bytes_written += n;
@@ -1052,6 +1072,15 @@ int zt_store_guided_filter(const char* in_path, const char* out_path, int dtype_
                            const char* encoding_json, float epsilon, int radius, int device,
                            int64_t row_begin, int64_t row_end, int nthreads, int flags,
                            zt_store_stats* stats) {
+    return zt_store_guided_filter_box(in_path, out_path, dtype_out, encoding_json, epsilon,
+                                      radius, device, row_begin, row_end, 0, -1, nthreads, flags,
+                                      stats);
+}
+
+int zt_store_guided_filter_box(const char* in_path, const char* out_path, int dtype_out,
+                               const char* encoding_json, float epsilon, int radius, int device,
+                               int64_t row_begin, int64_t row_end, int64_t col_begin,
+                               int64_t col_end, int nthreads, int flags, zt_store_stats* stats) {
     try {
         if (!in_path || !out_path) return zt::set_last_error(ZT_ERR_INVALID_PARAMETERS, "null path");
         if (radius < 0 || radius > 127)
@@ -1080,23 +1109,45 @@ int zt_store_guided_filter(const char* in_path, const char* out_path, int dtype_
             // of non-direct element types
             return (uint64_t)planes * plane * ((nd == 3 && radius <= 8) ? 8 : 20);
         };
+        // an output window of chunk columns along axis 1 (config T's (t, z) blocks,
+        // shard.block_assignment): its input carries the halo along axis 1 too
+        ColWin win{};
+        const bool windowed = nd >= 2 && col_end >= 0;
+        if (windowed) {
+            const int64_t oc = out.chunk_shape[1], n1 = in.shape[1];
+            const int64_t ncol = (out.shape[1] + oc - 1) / oc;
+            const int64_t c0 = std::max<int64_t>(0, col_begin), c1 = std::min(col_end, ncol);
+            if (c0 >= c1) return ZT_OK;
+            win.o0 = c0 * oc;
+            win.o1 = std::min(c1 * oc, out.shape[1]);
+            win.i0 = std::max<int64_t>(0, win.o0 - halo);
+            win.i1 = std::min(n1, win.o1 + halo);
+            plane = plane / n1 * (win.i1 - win.i0);
+        }
         op.apply = [&](zt_ctx* c, const void* slab, int64_t in0, int64_t in1, void* o, int64_t z0,
                        int64_t z1) -> int {
-            if (nd == 3 && radius <= 8)
+            if (nd == 3 && radius <= 8 && !windowed)
                 return zt_guided_filter_apply_slab(c, din, slab, dt, o, shape.data(), in0,
                                                    in1 - in0, z0, z1 - z0, chunk.data(), epsilon,
                                                    radius);
-            // n-D: the slab is a block whose windows clamp exactly where the array's do (it
-            // carries the halo or reaches the edge), so apply_ndarray on it is the chunked result
+            // n-D (or a window): the slab is a block whose windows clamp exactly where the
+            // array's do (it carries the halo or reaches the edge on every cut axis), so
+            // apply_ndarray on it is the chunked result
             std::vector<int64_t> bshape(shape), ostart(nd, 0), oshape(shape);
             bshape[0] = in1 - in0;
             ostart[0] = z0 - in0;
             oshape[0] = z1 - z0;
+            if (windowed) {
+                bshape[1] = win.i1 - win.i0;
+                ostart[1] = win.o0 - win.i0;
+                oshape[1] = win.o1 - win.o0;
+            }
             return zt_guided_filter_apply_ndarray(c, din, slab, bshape.data(), nullptr, nd,
                                                   ostart.data(), oshape.data(), dt, o, nullptr,
                                                   epsilon, radius);
         };
-        run_pipeline(in, out, device, row_begin, row_end, nthreads, op, stats);
+        run_pipeline(in, out, device, row_begin, row_end, nthreads, op, stats,
+                     windowed ? &win : nullptr);
         if (flags & ZT_STORE_FINISH_OUTPUT) out.store_metadata();
         return ZT_OK;
     } catch (const std::exception& e) {

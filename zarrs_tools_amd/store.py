@@ -270,16 +270,20 @@ def _flags(erase: bool, finish: bool) -> int:
 def guided_filter(input_path, output_path, epsilon: float, radius: int,
                   data_type: Optional[str] = None, device: int = 0, rows=None,
                   nthreads: int = 0, erase: bool = True, finish: bool = True,
-                  encoding=None, chunk_limit: int = 0) -> dict:
+                  encoding=None, chunk_limit: int = 0, cols=None) -> dict:
     """zarrs_filter guided-filter INPUT OUTPUT EPSILON RADIUS [--data-type T] on GPU `device`.
-    `rows` = (begin, end) output chunk rows along axis 0 (None = all); `chunk_limit` = at most
-    that many chunks in flight (--chunk-limit, 0 = memory-bounded). Returns the run stats."""
+    `rows` = (begin, end) output chunk rows along axis 0 (None = all); `cols` = (begin, end)
+    output chunk columns along axis 1 (None = all; a (t, z) block of a multi-GPU split);
+    `chunk_limit` = at most that many chunks in flight (--chunk-limit, 0 = memory-bounded).
+    Returns the run stats."""
     set_chunk_limit(chunk_limit)
     st = _abi.StoreStats()
     r0, r1 = (0, -1) if rows is None else (int(rows[0]), int(rows[1]))
-    check(lib().zt_store_guided_filter(_b(input_path), _b(output_path), _dt(data_type),
-                                       _enc(encoding), float(epsilon), int(radius), int(device), r0, r1,
-                                       int(nthreads), _flags(erase, finish), ctypes.byref(st)))
+    c0, c1 = (0, -1) if cols is None else (int(cols[0]), int(cols[1]))
+    check(lib().zt_store_guided_filter_box(_b(input_path), _b(output_path), _dt(data_type),
+                                           _enc(encoding), float(epsilon), int(radius),
+                                           int(device), r0, r1, c0, c1, int(nthreads),
+                                           _flags(erase, finish), ctypes.byref(st)))
     return st.as_dict()
 
 

@@ -419,11 +419,14 @@ def _rows_worker(name: str, src: str, dst: str, params: dict, device: int, rows,
     no metadata writes (the parent writes zarr.json once every row is done). `env`: the memory
     budget of this process (ZT_STORE_HOST_MEMORY / ZT_STORE_DEVICE_MEMORY, its share)."""
     os.environ.update(env or {})
+    cols = None
+    if isinstance(rows, tuple) and len(rows) == 2 and isinstance(rows[0], tuple):
+        rows, cols = rows  # ((row range), (column range)): a (t, z) block
     kw = dict(device=device, rows=rows, nthreads=nthreads, erase=False, finish=False,
               encoding=params.get("encoding"), data_type=params.get("data_type"),
               chunk_limit=params.get("chunk_limit") or 0)
     if name == "guided_filter":
-        return S.guided_filter(src, dst, params["epsilon"], params["radius"], **kw)
+        return S.guided_filter(src, dst, params["epsilon"], params["radius"], cols=cols, **kw)
     if name == "gaussian":
         return S.gaussian(src, dst, params["sigma"], params["kernel_half_size"], **kw)
     if name == "downsample_gaussian":  # a zarrs_ome level with --gaussian-sigma
@@ -447,6 +450,20 @@ def run_rows_parallel(name: str, src: str, dst: str, params: dict, out_shape, gp
     os.remove(os.path.join(dst, "zarr.json"))  # "not finished" until every row is written
     nrows = -(-out.shape[0] // out.chunk_shape[0])
     bounds = [(g * nrows // gpus, (g + 1) * nrows // gpus) for g in range(gpus)]
+    if name == "guided_filter" and len(out.shape) >= 4 and gpus > 1:
+        # 4-D series (config T): (t, z) blocks of whole chunks that minimise the input the
+        # processes decode and filter in all, halo included (shard.block_split): rows along t
+        # alone would make each process decode 3x its output timepoints
+        from . import shard
+        halo = (2 * int(params["radius"])) & 0xFF
+        groups = shard.block_split(gpus, out.shape, out.chunk_shape, halo)
+        if groups[1] > 1:
+            ncol = -(-out.shape[1] // out.chunk_shape[1])
+            bounds = []
+            for g in range(gpus):
+                k0, k1 = g // groups[1], g % groups[1]
+                bounds.append(((k0 * nrows // groups[0], (k0 + 1) * nrows // groups[0]),
+                               (k1 * ncol // groups[1], (k1 + 1) * ncol // groups[1])))
     devices = devices or list(range(gpus))
     per = max(1, (nthreads or min(16, os.cpu_count() or 1)) // gpus)
     params = dict(params)
@@ -466,9 +483,13 @@ def run_rows_parallel(name: str, src: str, dst: str, params: dict, out_shape, gp
         envs.append(env)
     t0 = time.perf_counter()
     with ProcessPoolExecutor(gpus, mp_context=mp.get_context("spawn")) as ex:
+        def nonempty(b):
+            if isinstance(b[0], tuple):
+                return b[0][1] > b[0][0] and b[1][1] > b[1][0]
+            return b[1] > b[0]
         futs = [ex.submit(_rows_worker, name, src, dst, params, devices[g], bounds[g], per,
                           envs[g])
-                for g in range(gpus) if bounds[g][1] > bounds[g][0]]
+                for g in range(gpus) if nonempty(bounds[g])]
         parts = [f.result() for f in futs]
     S.create_output(src, dst, params.get("data_type"), out_shape, params.get("encoding"))
     st = {k: sum(p[k] for p in parts) for k in parts[0] if isinstance(parts[0][k], (int, float))}
