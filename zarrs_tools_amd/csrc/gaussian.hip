@@ -11,6 +11,8 @@
 // input windows in LDS so each element is fetched about once (column and row kernels below).
 
 #include <hip/hip_runtime.h>
+
+#include <cstdlib>
 #include <stdint.h>
 
 #include <algorithm>
@@ -612,6 +614,226 @@ bool gaussian_zyx_supported(const GaussZYX& p, int dtype_in) {
 // (profiles/r03_gauss_variants_*.txt), identical output.
 struct ZYXWide { static constexpr int TY = 32, TX = 256, NT = 1024; };
 
+// ---------------------------------------------------------------------------------------------
+// gauss_zyx_kernel with the entering slice staged by LDS-DMA (round 4; f32 input, wide tiles,
+// whole-quad accesses): each wave issues its share of the staged tile's 1 KiB pieces as
+// `buffer_load_dwordx4 ... lds` from inline asm into one of two LDS slots, so the next slice's
+// bytes are in flight without holding VGPRs (the L-slice register ring fills them) and hipcc's
+// waitcnt pass, which does not see an asm load, never drains them: this kernel counts them with
+// its own `s_waitcnt vmcnt(N)` (cdna_hip_programming.md §5.7). Per step k:
+//   ring <- pre (slice k + MID, read from its slot during step k-1) ; z pass -> tile ;
+//   barrier 1 ; DMA of slice k + 2 + MID into the slot step k-1 read ; y pass -> ybuf ;
+//   own DMA of slice k + 1 + MID landed (vmcnt) ; barrier 2 ; pre <- that slot ; x pass, stores.
+// Same arithmetic, in the same order, as gauss_zyx_kernel: bit-identical output.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ void zdma16(zrsrc_t r, int voff, unsigned lds) {
+    unsigned keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %2\n\t"
+        "s_nop 0\n\t"
+        "buffer_load_dwordx4 %1, %3, 0 offen lds\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(voff), "s"(lds), "s"(r)
+        : "memory");
+}
+template <int N>
+__device__ __forceinline__ void zwait_vm() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+
+template <int L>
+__global__ __launch_bounds__(1024) void gauss_zyx_dma_kernel(const float* __restrict__ in,
+                                                             float* __restrict__ out, GaussZYX p,
+                                                             int tiles_x, int tiles_y, int zseg) {
+    using CFG = ZYXWide;
+    constexpr int TY = CFG::TY, TX = CFG::TX, NT = CFG::NT;
+    constexpr int TH = TY + L - 1, TW = TX + L - 1, MID = L / 2;
+    constexpr int MG = (MID + 3) / 4 * 4;
+    constexpr int TP = TX + 2 * MG, NQX = TP / 4;
+    constexpr int NQ = TH * NQX, NPQ = (NQ + NT - 1) / NT;
+    constexpr int NJ = (NQ + 63) / 64;  // 1 KiB DMA pieces per slice
+    constexpr int NXI = TY * (TX / 4), NXP = (NXI + NT - 1) / NT;
+    constexpr int NYI = TW * (TY / 4), NYP = (NYI + NT - 1) / NT;
+    static_assert(NXI % NT == 0, "every thread stores NXP quads per step (vmcnt count)");
+    static_assert(NPQ == 3 && NJ > 32 && NJ <= 48, "three pieces for waves < NJ - 32, else two");
+    __shared__ __attribute__((aligned(16))) float tile[NQ * 4];
+    __shared__ float ybuf[TY * TW];
+    __shared__ __attribute__((aligned(1024))) float slot[2][NJ * 256];
+    const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const bool three = wave + 32 < NJ;  // this wave issues a third piece (wave-uniform)
+    const int64_t nz = p.n[0], ny = p.n[1], nx = p.n[2];
+    const int64_t onz = p.on[0], ony = p.on[1], onx = p.on[2];
+    const int nwg = gridDim.x, b = blockIdx.x;
+    const int lid = (nwg % 8 == 0) ? (b % 8) * (nwg / 8) + b / 8 : b;
+    const int ntiles = tiles_x * tiles_y;
+    const int tile_i = lid % ntiles, seg = lid / ntiles;
+    const int64_t x0 = (int64_t)(tile_i % tiles_x) * TX, y0 = (int64_t)(tile_i / tiles_x) * TY;
+    const int64_t kz0 = (int64_t)seg * zseg, kz1 = kz0 + zseg < onz ? kz0 + zseg : onz;
+    const int hy = (int)(ony - y0 < TY ? ony - y0 : TY);
+    const int hx = (int)(onx - x0 < TX ? onx - x0 : TX);
+    const int64_t qy0 = p.o0[1] + y0 - MID, qx4 = p.o0[2] + x0 - MG;
+    const int64_t plane = ny * nx;
+    const uint32_t plane_bytes = (uint32_t)(plane * 4);
+    const uint32_t oplane_bytes = (uint32_t)(ony * onx * 4);
+    const unsigned slot_base = (unsigned)(uintptr_t)&slot[0][0];
+    int off[NPQ];
+    const bool edgex = qx4 < 0 || qx4 + TP > nx;
+    int bl = 0, br = 0;
+#pragma unroll
+    for (int k = 0; k < NPQ; ++k) {
+        const int q = tid + NT * k;
+        const int r = q / NQX, cq = q - r * NQX;
+        int64_t qy = qy0 + r;
+        qy = qy < 0 ? 0 : (qy > ny - 1 ? ny - 1 : qy);
+        int64_t xs = qx4 + 4 * cq;
+        bl |= xs < 0 ? 1 << k : 0;
+        br |= xs > nx - 4 ? 1 << k : 0;
+        xs = xs < 0 ? 0 : (xs > nx - 4 ? nx - 4 : xs);
+        off[k] = q < NQ ? (int)((qy * nx + xs) * 4) : kZBad;
+    }
+    auto fix = [&](float (&v)[NPQ][4]) {
+        if (edgex) {
+#pragma unroll
+            for (int k = 0; k < NPQ; ++k) {
+                const bool l = (bl >> k) & 1, rr = (br >> k) & 1;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[k][e] = l ? v[k][0] : (rr ? v[k][3] : v[k][e]);
+            }
+        }
+    };
+    for (int64_t o = blockIdx.y; o < p.outer; o += gridDim.y) {
+        const char* vol = reinterpret_cast<const char*>(in) + o * nz * plane * 4;
+        auto rs_of = [&](int64_t zq) {
+            zq = zq < 0 ? 0 : (zq > nz - 1 ? nz - 1 : zq);
+            return z_rsrc(vol + zq * plane * 4, plane_bytes);
+        };
+        // this wave's pieces of slice zq into slot sl: piece j = wave + 16 k carries quads
+        // [64 j, 64 j + 64), i.e. lane l's own quad tid + NT k
+        auto dma = [&](int64_t zq, int sl) {
+            const zrsrc_t rs = rs_of(zq);
+            const unsigned base = slot_base + (unsigned)sl * (NJ * 1024u);
+            zdma16(rs, off[0], base + (unsigned)wave * 1024u);
+            zdma16(rs, off[1], base + (unsigned)(wave + 16) * 1024u);
+            if (three) zdma16(rs, off[2], base + (unsigned)(wave + 32) * 1024u);
+        };
+        auto from_slot = [&](int sl, float (&v)[NPQ][4]) {
+            const float* sb = &slot[0][0] + sl * (NJ * 256);
+#pragma unroll
+            for (int k = 0; k < NPQ; ++k) {
+                const int q = tid + NT * k;
+                const float4 f = *reinterpret_cast<const float4*>(sb + 4 * (q < NJ * 64 ? q : 0));
+                v[k][0] = f.x; v[k][1] = f.y; v[k][2] = f.z; v[k][3] = f.w;
+            }
+        };
+        float ring[L][NPQ][4], pre[NPQ][4];
+        // window of the first output slice: slices o0 + kz0 + i - MID, i < L - 1, by plain loads
+#pragma unroll
+        for (int i = 0; i < L - 1; ++i) {
+            const zrsrc_t rs = rs_of(p.o0[0] + kz0 + i - MID);
+#pragma unroll
+            for (int k = 0; k < NPQ; ++k) z_load4<float>(rs, off[k], ring[i][k]);
+            fix(ring[i]);
+        }
+        // slice of window position L - 1 of step kz0 into slot 0, of step kz0 + 1 into slot 1
+        dma(p.o0[0] + kz0 + L - 1 - MID, 0);
+        zwait_vm<0>();
+        z_lds_barrier();
+        from_slot(0, pre);
+        dma(p.o0[0] + kz0 + L - MID, 1);
+        // NXP dropped stores, so that the first step's wait counts the same ops as every later
+        // step's (the previous step's stores, then this step's pieces)
+        {
+            const zrsrc_t none = z_rsrc(out, 0u);
+#pragma unroll
+            for (int ip = 0; ip < NXP; ++ip) __builtin_amdgcn_raw_buffer_store_b32(0u, none, kZBad, 0, 2);
+        }
+        char* obase = reinterpret_cast<char*>(out) + o * onz * ony * onx * 4;
+        for (int64_t kb = kz0; kb < kz1; kb += L) {
+            static_for<0, L>([&](auto PH_) {
+                constexpr int PH = decltype(PH_)::value;  // ring phase
+                const int64_t kz = kb + PH;
+                const int SL = (int)((kz - kz0) & 1);  // slot that held pre (wave-uniform)
+#pragma unroll
+                for (int k = 0; k < NPQ; ++k)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) ring[(PH + L - 1) % L][k][e] = pre[k][e];
+                fix(ring[(PH + L - 1) % L]);
+#pragma unroll
+                for (int k = 0; k < NPQ; ++k) {
+                    float sv[4];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        float sum = -0.0f;  // Iterator::sum::<f32> (kernel.rs:46, :66)
+#pragma unroll
+                        for (int i = 0; i < L; ++i)
+                            sum = sum + ring[(PH + i) % L][k][e] * p.w[0][i];
+                        sv[e] = sum;
+                    }
+                    const int q = tid + NT * k;
+                    if (k < NPQ - 1 || q < NQ)
+                        *reinterpret_cast<float4*>(tile + 4 * q) = make_float4(sv[0], sv[1], sv[2], sv[3]);
+                }
+                z_lds_barrier();
+                // slot SL (read into pre during the previous step) is free: the slice of window
+                // position L - 1 two steps on (clamped; unused past the segment)
+                dma(p.o0[0] + kz + 2 + L - 1 - MID, SL);
+#pragma unroll
+                for (int ip = 0; ip < NYP; ++ip) {
+                    const int item = tid + NT * ip;
+                    if (NYI % NT == 0 || item < NYI) {
+                        const int c = item % TW, r0 = (item / TW) * 4;
+                        float v[4 + L - 1];
+#pragma unroll
+                        for (int j = 0; j < 4 + L - 1; ++j) v[j] = tile[(r0 + j) * TP + c + MG - MID];
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) {
+                            float sum = -0.0f;
+#pragma unroll
+                            for (int i = 0; i < L; ++i) sum = sum + v[k + i] * p.w[1][i];
+                            ybuf[(r0 + k) * TW + c] = sum;
+                        }
+                    }
+                }
+                // own pieces of the next step's slice (issued a step ago, slot 1 - SL) landed:
+                // younger are the previous step's NXP stores and this step's pieces
+                if (three) zwait_vm<NXP + 3>(); else zwait_vm<NXP + 2>();
+                z_lds_barrier();
+                from_slot(1 - SL, pre);
+                const zrsrc_t ro = z_rsrc(obase + (kz < kz1 ? kz : 0) * ony * onx * 4,
+                                          kz < kz1 ? oplane_bytes : 0u);
+#pragma unroll
+                for (int ip = 0; ip < NXP; ++ip) {
+                    const int item = tid + NT * ip;
+                    const int r = item / (TX / 4), c0 = (item % (TX / 4)) * 4;
+                    const bool live = r < hy;
+                    float v[4 + L - 1];
+#pragma unroll
+                    for (int j = 0; j < 4 + L - 1; ++j) v[j] = ybuf[(live ? r : 0) * TW + c0 + j];
+                    float o4[4];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        float sum = -0.0f;
+#pragma unroll
+                        for (int i = 0; i < L; ++i) sum = sum + v[k + i] * p.w[2][i];
+                        o4[k] = sum;
+                    }
+                    const int ooff = (int)(((y0 + r) * onx + x0 + c0) * 4);
+                    typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+                    const u4 q = {__float_as_uint(o4[0]), __float_as_uint(o4[1]),
+                                  __float_as_uint(o4[2]), __float_as_uint(o4[3])};
+                    __builtin_amdgcn_raw_buffer_store_b128(q, ro, live && c0 < hx ? ooff : kZBad,
+                                                           0, 2);
+                }
+            });
+        }
+        zwait_vm<0>();  // no piece may land after the workgroup (or this volume) is done
+        z_lds_barrier();
+    }
+}
+
 template <int L, typename CFG>
 static hipError_t launch_zyx_cfg(const void* in, int dtype_in, float* out, const GaussZYX& p,
                                  bool quad, hipStream_t s) {
@@ -649,6 +871,26 @@ static hipError_t launch_zyx_cfg(const void* in, int dtype_in, float* out, const
 }
 
 template <int L>
+static hipError_t launch_zyx_dma(const float* in, float* out, const GaussZYX& p, hipStream_t s) {
+    using CFG = ZYXWide;
+    const int tiles_x = (int)((p.on[2] + CFG::TX - 1) / CFG::TX);
+    const int tiles_y = (int)((p.on[1] + CFG::TY - 1) / CFG::TY);
+    const int64_t tiles = (int64_t)tiles_x * tiles_y;
+    const int64_t outer = p.outer;
+    const int64_t per_launch = 2 * 256;  // as launch_zyx_cfg for one workgroup per CU
+    const int64_t want = (per_launch + tiles * outer - 1) / (tiles * outer);
+    int64_t nseg = std::max<int64_t>(1, std::min<int64_t>(want, (p.on[0] + kZYXSegMin - 1) / kZYXSegMin));
+    const int zseg = (int)((p.on[0] + nseg - 1) / nseg);
+    nseg = (p.on[0] + zseg - 1) / zseg;
+    const int64_t gx = tiles * nseg;
+    if (gx > 0x7FFFFFFF) return hipErrorInvalidValue;
+    const dim3 grid((unsigned)gx, (unsigned)(outer < 65535 ? outer : 65535));
+    hipLaunchKernelGGL((gauss_zyx_dma_kernel<L>), grid, dim3(CFG::NT), 0, s, in, out, p, tiles_x,
+                       tiles_y, zseg);
+    return hipGetLastError();
+}
+
+template <int L>
 static hipError_t launch_zyx_l(const void* in, int dtype_in, float* out, const GaussZYX& p,
                                hipStream_t s) {
     const int esz = dtype_size(dtype_in);
@@ -659,6 +901,15 @@ static hipError_t launch_zyx_l(const void* in, int dtype_in, float* out, const G
     // wide tiles when the march is a short quad march and the block is wide enough not to
     // leave most of a wide tile idle
     if constexpr (L <= 7) {
+        // f32 with whole-quad output rows: the entering slice staged by LDS-DMA
+        // (ZT_GAUSS_DMA=0 turns it off: A/B runs)
+        static const bool dma_off = [] {
+            const char* e = getenv("ZT_GAUSS_DMA");
+            return e && e[0] == '0';
+        }();
+        if (quad && p.on[2] >= ZYXWide::TX && dtype_in == kF32 && !dma_off &&
+            p.on[2] % 4 == 0 && ((uintptr_t)out & 15) == 0)
+            return launch_zyx_dma<L>(static_cast<const float*>(in), out, p, s);
         if (quad && p.on[2] >= ZYXWide::TX)
             return launch_zyx_cfg<L, ZYXWide>(in, dtype_in, out, p, quad, s);
     }

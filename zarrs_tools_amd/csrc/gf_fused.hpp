@@ -186,6 +186,9 @@ __device__ __forceinline__ int clamped_count(int i, int n, int r) {
     int hi = i + r > n - 1 ? n - 1 : i + r;
     return hi - lo + 1;
 }
+// Product of window counts (each <= 2R + 1 <= 17, products <= 17^3): the full-rate 24-bit
+// multiply instead of v_mul_lo_u32.
+__device__ __forceinline__ int cmul(int a, int b) { return (int)__umul24((unsigned)a, (unsigned)b); }
 
 template <int R, int K, typename T>
 __device__ __forceinline__ void core_window_sums(const T (&in)[K + 2 * R], T (&out)[K]) {
@@ -855,11 +858,11 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
         } else {
             const int gx = x0 - R + col;
             const bool xzin = gx >= 0 && gx < nx && zc >= 0 && zc < nz;
-            const int cxz = clamped_count(gx, nx, R) * clamped_count(zc, nz, R);
+            const int cxz = cmul(clamped_count(gx, nx, R), clamped_count(zc, nz, R));
 #pragma unroll
             for (int k = 0; k < NP3; ++k) {
                 const int gy = y0 - R + sg * C::K3 + 2 * k;
-                const int c0 = clamped_count(gy, ny, R) * cxz, c1 = clamped_count(gy + 1, ny, R) * cxz;
+                const int c0 = cmul(clamped_count(gy, ny, R), cxz), c1 = cmul(clamped_count(gy + 1, ny, R), cxz);
                 fc[k] = (f2){(float)c0, (float)c1};
                 rc[k] = (f2){rcp_tab[c0], rcp_tab[c1]};
             }
@@ -943,10 +946,10 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
 #pragma unroll
             for (int j = 0; j < K5; ++j) rc[j] = (f2){r, r};
         } else {
-            const int cxz = clamped_count(ox, nx, R) * clamped_count(zq, nz, R);
+            const int cxz = cmul(clamped_count(ox, nx, R), clamped_count(zq, nz, R));
 #pragma unroll
             for (int j = 0; j < K5; ++j) {
-                const float r = rcp_tab[clamped_count(oyb + j, ny, R) * cxz];
+                const float r = rcp_tab[cmul(clamped_count(oyb + j, ny, R), cxz)];
                 rc[j] = (f2){r, r};
             }
         }
