@@ -120,22 +120,34 @@ def test_p_pyramid_2048_u16_levels_bit_exact():
 
 
 def test_t_share_4d_sampled_chunks():
-    """Config T's real per-GPU share (output chunk rows along t): output
-    timepoints [8, 12) of the (32, 1024^3) series. The rank holds its input block, timepoints
-    [4, 16) = the output row plus the 2r t-halo, generated from the global synthetic definition
-    (zt_synth_box); every window clamps at the global array, which inside this block is the
-    block's own bounds (the halo is complete), so the middle chunk row of the block equals the
-    reference's per-chunk result of the global array."""
+    """Config T's real per-GPU share in the (t, z) block split of 8 GPUs
+    (shard.block_assignment, 2 t-groups x 4 z-rows): rank 5 owns output timepoints [16, 32) x
+    planes [256, 512) of the (32, 1024^3) series and holds its halo'd input block, timepoints
+    [12, 32) x planes [252, 516), generated from the global synthetic definition (zt_synth_box).
+    Every window clamps at the global array, which inside this block is the block's own bounds
+    on the cut axes (the halo is complete), so apply_ndarray on the block's output box equals the
+    reference's per-chunk result of the global array on sampled chunks (corner of the box, its
+    last chunk, an interior one)."""
     import torch
+    from zarrs_tools_amd import shard
     gshape, chunk, r = (32, 1024, 1024, 1024), (4, 256, 256, 256), 2
-    t0, tin = 4, 12
-    x = zt.synth_box((t0, 0, 0, 0), (tin,) + gshape[1:], gshape, kind="float32")
-    y = torch.zeros_like(x)
-    zt.GuidedFilter(EPS, r).apply(zt.DeviceArray(x, chunk), zt.DeviceArray(y, chunk),
-                                  chunk_grid_start=(1, 0, 0, 0), chunk_grid_count=(1, 4, 4, 4))
+    a = shard.block_assignment(5, 8, gshape, chunk, 2 * r, (2, 4))
+    assert a.out_start == (16, 256, 0, 0) and a.in_shape == (20, 264, 1024, 1024)
+    x = zt.synth_box(a.in_start, a.in_shape, gshape, kind="float32")
+    sub = zt.ArraySubset(tuple(o - i for o, i in zip(a.out_start, a.in_start)), a.out_shape)
+    y = zt.GuidedFilter(EPS, r).apply_ndarray(x, sub)
     torch.cuda.synchronize()
     del x
-    _check_chunks(y, gshape, chunk, r, [(2, 0, 0, 0), (2, 1, 2, 3), (2, 3, 3, 3)], z_off=t0)
+    coords = [(4, 1, 0, 0), (7, 1, 3, 3), (5, 1, 2, 1)]
+    refs = O.guided_filter_synth_chunks(gshape, chunk, coords, EPS, r, nthreads=16)
+    worst = 0.0
+    for (o0, osh, ref) in refs:
+        sl = tuple(slice(p - q, p - q + n) for p, q, n in zip(o0, a.out_start, osh))
+        got = y[sl].cpu().numpy()
+        d = np.abs(got.astype(np.float64) - ref) / np.maximum(1.0, np.abs(ref.astype(np.float64)))
+        worst = max(worst, float(d.max()))
+    print(f"config T share (t, z) block: max rel err {worst:.3e}")
+    assert worst <= FLOAT_TOL
 
 
 def test_2d_plane_of_2gib_routes_off_the_fused_path():

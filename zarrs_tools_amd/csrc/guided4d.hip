@@ -42,6 +42,8 @@ __device__ __forceinline__ void acc_add(double& a, double v) { a += v; }
 __device__ __forceinline__ void acc_sub(double& a, double v) { a -= v; }
 __device__ __forceinline__ void acc_add(dd2& a, const dd2& v) { a.x += v.x; a.y += v.y; }
 __device__ __forceinline__ void acc_sub(dd2& a, const dd2& v) { a.x -= v.x; a.y -= v.y; }
+__device__ __forceinline__ void acc_add(float2& a, float2 v) { a.x += v.x; a.y += v.y; }
+__device__ __forceinline__ void acc_sub(float2& a, float2 v) { a.x -= v.x; a.y -= v.y; }
 __device__ __forceinline__ void put(double& o, double a) { o = a; }
 __device__ __forceinline__ void put(float2& o, const dd2& a) { o = make_float2((float)a.x, (float)a.y); }
 template <typename TV> __device__ __forceinline__ TV zero_v();
@@ -428,6 +430,9 @@ __device__ __forceinline__ void store_dtype(void* out, int dtype, int64_t i, flo
 // K3f: one workgroup marches one 64 x kTY xy tile of the OUTPUT box through a z segment of it, for
 // one output timepoint; the running z-window (f64 pair) covers the tile's R apron, whose loads
 // reach into the block's halo (zero outside the block: the clamped windows).
+// K3f: one workgroup marches one 64 x kTY xy tile of the OUTPUT box through a z segment of it, for
+// one output timepoint; the running z-window (f64 pair) covers the tile's R apron, whose loads
+// reach into the block's halo (zero outside the block: the clamped windows).
 template <int R>
 __global__ __launch_bounds__(kNT) void box3_final_kernel(const float2* __restrict__ TAB,
                                                          const float* __restrict__ v,
@@ -436,8 +441,11 @@ __global__ __launch_bounds__(kNT) void box3_final_kernel(const float2* __restric
                                                          int tiles_y, Str3 vs) {
     constexpr int EX = kTX + 2 * R, EY = kTY + 2 * R, NE = EX * EY;
     constexpr int NPT = (NE + kNT - 1) / kNT;
-    __shared__ dd2 Z[EY][EX];
-    __shared__ dd2 X[EY][kTX];
+    // the running z-window is an f64 pair in registers (exact add / subtract); the x and y
+    // windows of it go through LDS as f32 pairs (stage 2 is rounded to f32 anyway: half the LDS
+    // bytes and f32 instead of f64 adds; the x / y sliding sums span kKX / kKY outputs only)
+    __shared__ float2 Z[EY][EX];
+    __shared__ float2 X[EY][kTX];
     const int T = (int)g.shape[0], nz = (int)g.shape[1], ny = (int)g.shape[2],
               nx = (int)g.shape[3];
     const int ot = blockIdx.y;
@@ -484,7 +492,7 @@ __global__ __launch_bounds__(kNT) void box3_final_kernel(const float2* __restric
         for (int k = 0; k < NPT; ++k) {
             acc_add(zs[k], pa[k]);
             acc_sub(zs[k], ps[k]);
-            if (ey_[k] >= 0) Z[ey_[k]][ex_[k]] = zs[k];
+            if (ey_[k] >= 0) Z[ey_[k]][ex_[k]] = make_float2((float)zs[k].x, (float)zs[k].y);
         }
 #pragma unroll
         for (int k = 0; k < NPT; ++k) {
@@ -494,8 +502,7 @@ __global__ __launch_bounds__(kNT) void box3_final_kernel(const float2* __restric
         __syncthreads();
         for (int it = threadIdx.x; it < EY * (kTX / kKX); it += kNT) {
             const int ey = it / (kTX / kKX), sx = (it % (kTX / kKX)) * kKX;
-            dd2 sacc;
-            acc_zero(sacc);
+            float2 sacc = make_float2(0.f, 0.f);
 #pragma unroll
             for (int j = 0; j <= 2 * R; ++j) acc_add(sacc, Z[ey][sx + j]);
             X[ey][sx] = sacc;
@@ -511,8 +518,7 @@ __global__ __launch_bounds__(kNT) void box3_final_kernel(const float2* __restric
             const int tx = threadIdx.x % kTX, sy = (threadIdx.x / kTX) * kKY;
             const int gx = x0 + tx;
             const int czx = ccount(z, nz, R) * ccount(gx, nx, R) * ct;
-            dd2 sacc;
-            acc_zero(sacc);
+            float2 sacc = make_float2(0.f, 0.f);
 #pragma unroll
             for (int j = 0; j <= 2 * R; ++j) acc_add(sacc, X[sy + j][tx]);
 #pragma unroll
