@@ -75,6 +75,9 @@ def main():
     ap.add_argument("--t", type=int, default=0,
                     help="4-D time series (config T): T timepoints of nz x size x size")
     ap.add_argument("--t-chunk", type=int, default=4, help="chunk extent along t (4-D)")
+    ap.add_argument("--procs", type=int, default=1,
+                    help="zarrs_filter --gpus N's store split (4-D: (t, z) blocks) over N "
+                         "processes, all on device 0 here (a one-GPU rehearsal)")
     ap.add_argument("--cpu-chunks", type=int, default=0,
                     help="also time the CPU store -> store baseline on this many output chunks")
     a = ap.parse_args()
@@ -95,7 +98,15 @@ def main():
         t_make = time.perf_counter() - t0
         stats = []
         for _ in range(a.repeat):
-            stats.append(S.guided_filter(pin, pout, a.eps, a.radius, nthreads=a.threads))
+            if a.procs > 1:
+                from zarrs_tools_amd.zarrs_filter import run_rows_parallel
+                st = run_rows_parallel("guided_filter", pin, pout,
+                                       {"epsilon": a.eps, "radius": a.radius}, shape, a.procs,
+                                       nthreads=a.threads, devices=[0] * a.procs)
+                st["threads"] = a.threads
+                stats.append(st)
+            else:
+                stats.append(S.guided_filter(pin, pout, a.eps, a.radius, nthreads=a.threads))
         best = min(stats, key=lambda s: s["wall_s"])
         vox = best["voxels"]
         res = {
@@ -104,7 +115,7 @@ def main():
             "unit": "GiB/s",
             "config": {"shape": shape, "chunk": chunk, "radius": a.radius, "eps": a.eps,
                        "codec": a.codec, "level": a.level, "shard_inner": a.shard_inner,
-                       "host_threads": best["threads"]},
+                       "host_threads": best["threads"], "processes": a.procs},
             "wall_s": round(best["wall_s"], 3),
             "phases": {k: round(best[k], 3) for k in
                        ("decode_s", "encode_s", "h2d_s", "kernel_s", "d2h_s")},

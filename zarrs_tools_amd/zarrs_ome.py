@@ -211,7 +211,7 @@ def _box_chunks(bstart, bshape, chunk, shape):
 
 
 def _octant_worker(out_root: str, assign, factor, discrete: bool, device: int, nthreads: int,
-                   scratch: str, env=None, compute=None) -> dict:
+                   scratch: str, env=None, compute=None, src0=None) -> dict:
     """One process of `zarrs_ome --gpus N` (SURVEY.md §8(e) octant ownership): read this rank's
     factor^L-aligned level-0 box into HBM, compute levels 1..L of the box there (the windows never
     cross an aligned box boundary), write every output chunk lying wholly inside the box, and
@@ -224,7 +224,8 @@ def _octant_worker(out_root: str, assign, factor, discrete: bool, device: int, n
           "voxels": 0}
     if assign.coord is None or assign.local_levels == 0:
         return st
-    lvl0 = os.path.join(out_root, "0")
+    # level 0: the output's copy, or the input itself while the parent is still copying it
+    lvl0 = src0 or os.path.join(out_root, "0")
     info0 = S.open_array(lvl0)
     if compute is None:
         import torch
@@ -296,18 +297,21 @@ def _octant_worker(out_root: str, assign, factor, discrete: bool, device: int, n
     return st
 
 
-def prepare_octant_levels(out_root: str, level_shapes, local_levels: int) -> None:
+def prepare_octant_levels(out_root: str, level_shapes, local_levels: int, src0=None) -> None:
     """Create the level arrays 1..local_levels (each from the previous level's encoding,
-    zarrs_ome.rs:528-560) with their metadata pending until every chunk is written."""
+    zarrs_ome.rs:528-560; level 0's encoding from `src0` when given) with their metadata pending
+    until every chunk is written."""
     for i in range(1, local_levels + 1):
         src, dst = os.path.join(out_root, str(i - 1)), os.path.join(out_root, str(i))
+        if i == 1 and src0:
+            src = src0
         S.create_output(src, dst, None, level_shapes[i - 1],
                         level_encoding(S.open_array(src), level_shapes[i - 1]))
         _hold_metadata(dst)
 
 
 def run_octants(out_root: str, shape0, factor, levels, discrete: bool, gpus: int, devices=None,
-                nthreads: int = 0, log=print, compute=None):
+                nthreads: int = 0, log=print, compute=None, src0=None):
     """Levels 1..L of the pyramid over `gpus` processes, one per GPU, each owning a factor^L-
     aligned box of level 0 (shard.octant_assignment; no exchange between processes). The level
     arrays 1..L must exist with pending metadata; chunks crossing box boundaries are assembled
@@ -326,7 +330,7 @@ def run_octants(out_root: str, shape0, factor, levels, discrete: bool, gpus: int
     try:
         with ProcessPoolExecutor(gpus, mp_context=mp.get_context("spawn")) as ex:
             futs = [ex.submit(_octant_worker, out_root, assigns[g], list(factor), discrete,
-                              devices[g], per, scratch, envs[g], compute)
+                              devices[g], per, scratch, envs[g], compute, src0)
                     for g in range(gpus) if assigns[g].coord is not None]
             parts = [f.result() for f in futs]
         t1 = time.perf_counter()
@@ -415,6 +419,7 @@ def run(input_path, output_path, factor=None, max_levels: int = 10, discrete: bo
     on_device = (not multi and device_resident and _device_ok(device)
                  and _device_pyramid_fits(info0, gauss, device))
     cur = None  # the previous level in HBM (device-resident pyramid)
+    copy_thread, copy_err = None, []
     if reencoding:
         _reencode_level0(input_path, lvl0, reencoding, nthreads, log, device)
     else:
@@ -424,18 +429,40 @@ def run(input_path, output_path, factor=None, max_levels: int = 10, discrete: bo
         # pyramid streams the same input into HBM meanwhile (the copy's reads warm the page
         # cache for it, or the other way round), so level 0 costs one pass over the input
         import threading
-        copy_err = []
 
         def _copy():
             try:
                 shutil.copytree(input_path, lvl0)
             except BaseException as e:  # re-raised below
                 copy_err.append(e)
-        th = threading.Thread(target=_copy)
-        th.start()
+        copy_thread = threading.Thread(target=_copy)
+        copy_thread.start()
         if on_device:
             cur, on_device = _ingest(input_path, device, nthreads, log)
-        th.join()
+    octants_done = 0  # levels 1..octants_done computed by run_octants
+    stats = []
+    if multi and gauss is None and level_shapes:
+        # octant-owned levels on one process per GPU; without reencoding their level 0 is the
+        # input itself, so they start while this process is still copying it to level 0
+        from . import shard
+        src0 = input_path if not reencoding else lvl0
+        devices = list(gpu_devices or range(gpus))[:gpus]
+        boxes = [shard.octant_assignment(g, gpus, info.shape, factor, len(level_shapes))
+                 for g in range(gpus)]
+        big = max(boxes, key=lambda b: int(np.prod(b.shape)))
+        box_info = S.ArrayInfo(src0, dt0, tuple(big.shape), (), ())
+        # every distinct device must hold its processes' boxes (each with its own count)
+        fits = all(_device_pyramid_fits(box_info, None, d, sharing=devices.count(d),
+                                        host_share=gpus) for d in sorted(set(devices)))
+        if big.local_levels > 0 and fits:
+            prepare_octant_levels(output_path, level_shapes, big.local_levels, src0)
+            octants_done, st_oct = run_octants(output_path, list(info.shape), factor,
+                                               len(level_shapes), discrete, gpus, devices,
+                                               nthreads, log, src0=src0)
+            st_oct["levels"] = octants_done
+            stats.append(st_oct)
+    if copy_thread is not None:
+        copy_thread.join()
         if copy_err:
             raise copy_err[0]
         log(f"0: copy {input_path} -> {lvl0} ({info.data_type} {list(info.shape)})")
@@ -457,25 +484,6 @@ def run(input_path, output_path, factor=None, max_levels: int = 10, discrete: bo
     datasets = [{"path": "0", "coordinateTransformations": [
         {"type": "scale", "scale": list(scale)}]}]
     shape = list(S.open_array(lvl0).shape)
-    stats = []
-    lvl0_info = S.open_array(lvl0)
-    octants_done = 0  # levels 1..octants_done computed by run_octants
-    if multi and gauss is None and level_shapes:
-        from . import shard
-        devices = list(gpu_devices or range(gpus))[:gpus]
-        boxes = [shard.octant_assignment(g, gpus, shape, factor, len(level_shapes))
-                 for g in range(gpus)]
-        big = max(boxes, key=lambda b: int(np.prod(b.shape)))
-        box_info = S.ArrayInfo(lvl0, lvl0_info.data_type, tuple(big.shape), (), ())
-        # every distinct device must hold its processes' boxes (each with its own count)
-        fits = all(_device_pyramid_fits(box_info, None, d, sharing=devices.count(d),
-                                        host_share=gpus) for d in sorted(set(devices)))
-        if big.local_levels > 0 and fits:
-            prepare_octant_levels(output_path, level_shapes, big.local_levels)
-            octants_done, st_oct = run_octants(output_path, shape, factor, len(level_shapes),
-                                               discrete, gpus, devices, nthreads, log)
-            st_oct["levels"] = octants_done
-            stats.append(st_oct)
     fused_levels = None  # every level of the device-resident mean / mode pyramid, one call
     if on_device:
         from . import filter as F
