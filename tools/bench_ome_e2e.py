@@ -62,6 +62,11 @@ def main():
             res[mode] = {"wall_s": round(wall, 3), "levels": r["levels"],
                          "input_gvox_per_s": round(a.size ** 3 / wall / 1e9, 3),
                          "level_s": [round(st["wall_s"], 3) for st in r["stats"]]}
+            oct_st = [st for st in r["stats"] if "per_rank" in st]
+            if oct_st:  # the octant workers' own phases (box read, device pyramid, writes)
+                res[mode]["octant_ranks"] = [
+                    {k: (round(v, 3) if isinstance(v, float) else v) for k, v in pr.items()}
+                    for pr in oct_st[0]["per_rank"]]
             for lvl, want in enumerate(refs[:r["levels"]], start=1):
                 got = S.read_array(os.path.join(out, str(lvl)), (0, 0, 0), want.shape)
                 ok = ok and bool(np.array_equal(got, want))

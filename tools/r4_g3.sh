@@ -10,4 +10,4 @@ timeout -k 10 400 python -u tools/bench_ops.py --only tshare --reps 3 --t-groups
 ZT_G4_LEGACY=1 timeout -k 10 400 python -u tools/bench_ops.py --only tshare --reps 3 --t-groups 2 4 >> gpurun_out/r4_tshare2.jsonl 2>> gpurun_out/r4_tshare2.err
 cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/r4_tshare_prof -o run -- python3 $GRAFT_REPO_ROOT/tools/bench_ops.py --only tshare,gaussian --reps 2 --t-groups 2 4 > /dev/null 2>&1
 cd $GRAFT_REPO_ROOT/tools/bin
-for v in tk_base tk_u24 tk_base tk_u24; do timeout -k 10 90 ./$v 2048 $v 512 >> $GRAFT_REPO_ROOT/gpurun_out/r4_tk2.txt; done
+for v in tk_u24 tk_seed tk_u24 tk_seed; do timeout -k 10 90 ./$v 2048 $v 512 >> $GRAFT_REPO_ROOT/gpurun_out/r4_tk2.txt; done
