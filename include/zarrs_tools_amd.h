@@ -67,9 +67,9 @@ size_t zt_dtype_size(int dtype);
 /* Number of HIP devices visible (0 on a host without GPUs; never an error). */
 int zt_device_count(int* count);
 /* Fused guided-filter kernel selection (process-wide, no reference analogue): 0 = the default
- * gf3d_fused_kernel, the only variant in this library; the measured-slower designs (the
- * single-barrier gf_v9.hpp, gf_v3.hpp) are built only by tools/ for A/B timing, and any other
- * value is rejected here. Returns the previous value. */
+ * gf3d_fused_kernel, the only variant built (the measured-slower designs of rounds 2-3 were
+ * deleted; DESIGN.md §3.1 keeps their numbers); any other value is rejected. Returns the
+ * previous value. */
 int zt_set_fused_variant(int variant);
 
 /* One context per (host thread, device): owns a HIP stream, events and reusable scratch. */

@@ -15,7 +15,7 @@
 #include "zt_kernels.hpp"
 
 // Tuning knobs (tools/timek.hip sweeps them with -D; profiles/r02_ab_harness.txt). Variants that
-// were measured slower live only in tools/gf_fused_variants.hpp.
+// were measured slower were deleted; their numbers stay in DESIGN.md §3.1.
 #ifndef GF_K4_R4
 #define GF_K4_R4 8  // r = 4: P4 outputs per item (8 x per item, -2 %)
 #endif

@@ -379,9 +379,6 @@ const char* zt_last_error(void) { return g_last_error.c_str(); }
 size_t zt_dtype_size(int dtype) { return zt::dtype_size(dtype); }
 
 int zt_set_fused_variant(int variant) {
-    if (variant == 1)
-        return fail(ZT_ERR_INVALID_PARAMETERS,
-                    "fused variant 1 (gf_v9.hpp) is built only by tools/ (A/B timing), not here");
     if (variant != 0) return fail(ZT_ERR_INVALID_PARAMETERS, "fused variant must be 0");
     return zt::fused_variant().exchange(variant);
 }

@@ -32,8 +32,6 @@ struct GFParams {
     int itx0, itx1, ity0, ity1;  // interior tile range (fused kernel, host-computed)
     float eps;
     float rcp_w3;  // RN(1 / (2r+1)^3): the interior window count's reciprocal (host-computed)
-    unsigned long long* trace;  // tools/trace_steps only (tools/gf_fused_variants.hpp): per-step clock stamps of one workgroup; unused by the product kernels
-    int trace_block;
 };
 
 // N-d geometry for the separable path and downsample (C-order logical shapes).
@@ -49,7 +47,7 @@ struct NdGeom {
 };
 
 bool fused_supports_radius(int radius);
-// process-wide fused-kernel selection (zt_set_fused_variant): 0 default, 1 gf_v9.hpp
+// process-wide fused-kernel selection (zt_set_fused_variant): only 0, the default, is built
 std::atomic<int>& fused_variant();
 int fused_tile_y(int radius);  // output tile height of the fused kernel for this radius
 // element-type pairs with a direct fused instantiation; others are staged through f32
