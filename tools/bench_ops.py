@@ -181,7 +181,7 @@ def bench_t_share(reps, radius=2, groups=None, rank=None):
                        "output_box": [list(a.out_start), list(a.out_shape)],
                        "input_box": [list(a.in_start), list(a.in_shape)],
                        "dtype": "float32", "eps": 2500.0,
-                       "path": "one apply_ndarray call on the halo'd (t, z) block, four-kernel 4-D"},
+                       "path": "one apply_ndarray call on the halo'd (t, z) block: 4-D three-kernel form (box3_march_kernel, g4_tab_kernel, box3_final_kernel)"},
             "ms": round(ms, 4), "gib_per_s": round(n * 4 / 2 ** 30 / (ms / 1e3), 3),
             "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),

@@ -3,7 +3,8 @@
 the FETCH_SIZE / WRITE_SIZE passes of tools/profile_pmc.sh, keyed to the library build (sha256),
 the workload and the world size, so bench.py only reports it for the build it was measured on.
 
-Usage: make_traffic_json.py PMC_DIR OUT_JSON [size radius]  (merges into OUT_JSON's entries)
+Usage: make_traffic_json.py PMC_DIR OUT_JSON [size radius [G/N]]  (merges into OUT_JSON's entries;
+G/N keys the entry to a `bench.py --share G/N` proxy run)
 Method (MI355X_MICROARCH.md, HBM / rocprofv3): one launch (bench.py --steps 1 --warmup 0), each
 counter in its own run; FETCH_SIZE and WRITE_SIZE are KiB; FETCH_SIZE x2 is the gfx950
 correction for wide (128 B) reads counted as 64 B.
@@ -32,23 +33,32 @@ def main():
     pmc, out = sys.argv[1], sys.argv[2]
     size = int(sys.argv[3]) if len(sys.argv) > 3 else 2048
     radius = int(sys.argv[4]) if len(sys.argv) > 4 else 4
+    share = [int(v) for v in sys.argv[5].split("/")] if len(sys.argv) > 5 else None
     fetch, nf = total(os.path.join(pmc, "fetch"), "FETCH_SIZE")
     write, nw = total(os.path.join(pmc, "write"), "WRITE_SIZE")
-    if nf != 1 or nw != 1:
-        sys.exit(f"expected one launch per pass, got {nf} / {nw}")
+    # one step per pass: one launch, or the interior + edge launches of a share's slab
+    if nf != nw or not 1 <= nf <= 2:
+        sys.exit(f"expected the launches of one step per pass, got {nf} / {nw}")
     h = hashlib.sha256()
     with open(os.path.join(ROOT, "zarrs_tools_amd", "libzarrs_tools_amd.so"), "rb") as f:
         for blk in iter(lambda: f.read(1 << 20), b""):
             h.update(blk)
     vox = size ** 3
+    if share is not None:  # the voxels of that rank's slab (bench.py's slab_assignment)
+        sys.path.insert(0, ROOT)
+        from zarrs_tools_amd.shard import slab_assignment
+        a = slab_assignment(share[0], share[1], size, 256, 2 * radius)
+        vox = a.out_nz * size * size
     rd, wr = fetch * 1024 * 2, write * 1024
     d = {"lib_sha256": h.hexdigest(), "global_shape": [size] * 3, "radius": radius, "world": 1,
-         "kernel": "gf3d_fused_kernel (interior + edge launches of one step)",
+         "kernel": "gf3d_fused_kernel (interior + edge launches of one step)", "launches": nf,
          "hbm_bytes_per_launch": rd + wr, "read_bytes_per_voxel": round(rd / vox, 3),
          "write_bytes_per_voxel": round(wr / vox, 3),
          "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate runs of bench.py "
                    "--steps 1 --warmup 0; FETCH_SIZE x2 (gfx950 wide-read correction), KiB -> "
                    "bytes; Infinity-Cache hits are counted by these counters"}
+    if share is not None:
+        d["share"] = share
     # merge: one entry per (shape, radius, world); entries of other builds are dropped
     entries = []
     if os.path.exists(out):
@@ -58,8 +68,8 @@ def main():
         except ValueError:
             entries = []
     entries = [e for e in entries if e.get("lib_sha256") == d["lib_sha256"] and
-               (e.get("global_shape"), e.get("radius"), e.get("world", 1)) !=
-               (d["global_shape"], d["radius"], d["world"])]
+               (e.get("global_shape"), e.get("radius"), e.get("world", 1), e.get("share")) !=
+               (d["global_shape"], d["radius"], d["world"], d.get("share"))]
     entries.append(d)
     with open(out, "w") as f:
         json.dump({"entries": entries}, f, indent=1)

@@ -1,14 +1,16 @@
 #!/bin/bash
 # rocprofv3 counter passes for the guided-filter kernel (run on the GPU box from the repo root).
-# Usage: tools/profile_pmc.sh OUTDIR [bench args...]
+# Usage: [PASSES="fetch write"] tools/profile_pmc.sh OUTDIR [bench args...]
 # Each --pmc pass is its own run (kernel-trace only; no sys/runtime trace with counters).
 set -u
 OUT=$1; shift
 ROOT=$(pwd)
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
+PASSES=${PASSES:-"sq1 sq2 fetch write tcc"}
 run() {  # name counters...
   local name=$1; shift
+  [[ " $PASSES " == *" $name "* ]] || return 0
   timeout -k 10 240 rocprofv3 --pmc "$@" -d "$ROOT/$OUT/$name" -o run --output-format csv -- \
     python3 "$ROOT/bench.py" --no-cpu-baseline "${BENCH_ARGS[@]}" > "$ROOT/$OUT/$name.log" 2>&1
   echo "$name rc=$?"
