@@ -61,7 +61,10 @@
 #ifndef SK_STY
 #define SK_STY 16
 #endif
-constexpr int R = 4, TX = SK_TX, TY = 2048 / SK_TX, NT = 1024, STX = SK_STX, STY = SK_STY;
+#ifndef SK_TY
+#define SK_TY (2048 / SK_TX)  // tile height (64 x 16: half the co-resident L2 footprint per XCD)
+#endif
+constexpr int R = 4, TX = SK_TX, TY = SK_TY, NT = 1024, STX = SK_STX, STY = SK_STY;
 
 #define CK(x)                                                                              \
     do {                                                                                   \
@@ -244,8 +247,8 @@ int main(int argc, char** argv) {
         }
     }
     const double gb = (double)count * 8 / 1e9;
-    printf("skeleton LDIST=%d NOSTORE=%d ST=%dx%d PAD=%d,%d STAUX=%d SK_BAR=%d SK_PF=%d TX=%d M1=%d noleave=%d noP3=%d noP5=%d lds=%d n=%d wg=%d: mean %.3f ms min %.3f ms (%.1f GB/s algorithmic)\n",
-           SK_LDIST, SK_NOSTORE, STX, STY, SK_PADX, SK_PADY, SK_STAUX, SK_BAR, SK_PF, TX, SK_M1, SK_NOLEAVE, SK_NOP3, SK_NOP5, lds, n, nwg, sum / reps, best, gb / (sum / reps) * 1e3);
+    printf("skeleton TY=%d LDIST=%d NOSTORE=%d ST=%dx%d PAD=%d,%d STAUX=%d SK_BAR=%d SK_PF=%d TX=%d M1=%d noleave=%d noP3=%d noP5=%d lds=%d n=%d wg=%d: mean %.3f ms min %.3f ms (%.1f GB/s algorithmic)\n",
+           TY, SK_LDIST, SK_NOSTORE, STX, STY, SK_PADX, SK_PADY, SK_STAUX, SK_BAR, SK_PF, TX, SK_M1, SK_NOLEAVE, SK_NOP3, SK_NOP5, lds, n, nwg, sum / reps, best, gb / (sum / reps) * 1e3);
     CK(hipFree(in));
     CK(hipFree(out));
     CK(hipFree(dummy));

@@ -2,8 +2,10 @@
 // alike, guided_filter.rs:117-199 with get_block clamping on all four axes).
 //
 // The box mean over (t, z, y, x) is separable and linear, so the 4-D sums are t-window sums of
-// per-timepoint 3-D box sums:  box4(f)(t) = sum_{t' in W(t)} box3(f(t')).  Four kernels over the
-// halo'd block (windows clamp at the block bounds = the array bounds):
+// per-timepoint 3-D box sums:  box4(f)(t) = sum_{t' in W(t)} box3(f(t')). The default is three
+// kernels (K1, then g4_tab_kernel and box3_final_kernel, described above them); ZT_G4_LEGACY=1
+// keeps the original four over the halo'd block (windows clamp at the block bounds = the array
+// bounds):
 //   K1 box3_march<float -> double>:  U3(t) = 3-D window sums of v, exact f64 (f64 sums of f32
 //       values), one z-march per (timepoint, xy tile);
 //   K2 pointwise (all t of a voxel in one thread): U4 = t-window sums of U3 (exact),
@@ -71,10 +73,31 @@ struct Str3 {
     int64_t t, z, y;
 };
 
+// XCD-aware block order. Consecutive linear block ids are dispatched round-robin over the 8 XCDs
+// (each with its own L2); give each XCD a contiguous run of (tile, timepoint) ids instead, so the
+// workgroups resident on one XCD march neighbouring tiles whose aprons share that XCD's L2 lines.
+__device__ __forceinline__ void xcd_block(int& bx, int& by) {
+    const int64_t gx = gridDim.x, total = gx * gridDim.y;
+    const int64_t lin = blockIdx.x + (int64_t)blockIdx.y * gx;
+    const int64_t lid = total % 8 == 0 ? (lin % 8) * (total / 8) + lin / 8 : lin;
+    bx = (int)(lid % gx);
+    by = (int)(lid / gx);
+}
+
+// The z-window ring: with the last 2R + 1 entering slices of a thread's apron points held in
+// registers, the leaving slice of the running z-window is never re-read from memory (with ~8
+// resident workgroups per CU its lines are long gone from L2 by then; the T share's box3 marches
+// read 2-2.5x their compulsory bytes without the ring). Used when the ring fits in 64 VGPRs.
+template <int R, typename TV, int NPT>
+constexpr bool box3_ring() {
+    return NPT * (2 * R + 1) * (int)(sizeof(TV) / 4) <= 64;
+}
+
 // 3-D window sums (radius R, clamped to the volume) of every timepoint volume of a (T, nz, ny, nx)
 // C-order array: a workgroup marches one 64 x 16 xy tile through zseg slices of one timepoint.
 // Each thread keeps the running z-window of its points of the (tile + R) apron in registers
-// (entering and leaving slices prefetched a step ahead); x- then y-window sums go through LDS.
+// (the entering slice prefetched a step ahead; the leaving one from the ring, box3_ring, or
+// prefetched too); x- then y-window sums go through LDS.
 template <int R, typename TV, typename TA, typename TO>
 __global__ __launch_bounds__(kNT) void box3_march_kernel(const TV* __restrict__ in,
                                                          TO* __restrict__ out, int nz, int ny,
@@ -82,11 +105,13 @@ __global__ __launch_bounds__(kNT) void box3_march_kernel(const TV* __restrict__ 
                                                          int tiles_y, Str3 is) {
     constexpr int EX = kTX + 2 * R, EY = kTY + 2 * R, NE = EX * EY;
     constexpr int NPT = (NE + kNT - 1) / kNT;
+    constexpr int W = 2 * R + 1;
     __shared__ TA Z[EY][EX];
     __shared__ TA X[EY][kTX];
-    const int t = blockIdx.y;
+    int bx, t;
+    xcd_block(bx, t);
     const int ntile = tiles_x * tiles_y;
-    const int seg = blockIdx.x / ntile, tile = blockIdx.x % ntile;
+    const int seg = bx / ntile, tile = bx % ntile;
     const int x0 = (tile % tiles_x) * kTX, y0 = (tile / tiles_x) * kTY;
     const int z0 = seg * zseg, z1 = min(z0 + zseg, nz);
     const int64_t plane = (int64_t)ny * nx;
@@ -108,30 +133,8 @@ __global__ __launch_bounds__(kNT) void box3_march_kernel(const TV* __restrict__ 
     auto load = [&](int z, int k) -> TV {
         return (pidx[k] >= 0 && z >= 0 && z < nz) ? vol[(int64_t)z * is.z + pidx[k]] : zero_v<TV>();
     };
-    TA zs[NPT];
-#pragma unroll
-    for (int k = 0; k < NPT; ++k) {  // window of slice z0 - 1
-        acc_zero(zs[k]);
-        for (int z = z0 - 1 - R; z <= z0 - 1 + R; ++z) acc_add(zs[k], load(z, k));
-    }
-    TV pa[NPT], ps[NPT];
-#pragma unroll
-    for (int k = 0; k < NPT; ++k) {
-        pa[k] = load(z0 + R, k);
-        ps[k] = load(z0 - R - 1, k);
-    }
-    for (int z = z0; z < z1; ++z) {
-#pragma unroll
-        for (int k = 0; k < NPT; ++k) {
-            acc_add(zs[k], pa[k]);
-            acc_sub(zs[k], ps[k]);
-            if (ey_[k] >= 0) Z[ey_[k]][ex_[k]] = zs[k];
-        }
-#pragma unroll
-        for (int k = 0; k < NPT; ++k) {  // next step's entering / leaving slices
-            pa[k] = load(z + 1 + R, k);
-            ps[k] = load(z - R, k);
-        }
+    // x- and y-window sums of the Z slice of output slice z (the caller filled Z)
+    auto xy_windows = [&](int z) {
         __syncthreads();
         // x-window: EY rows x (kTX / kKX) segments of kKX outputs
         for (int it = threadIdx.x; it < EY * (kTX / kKX); it += kNT) {
@@ -150,25 +153,84 @@ __global__ __launch_bounds__(kNT) void box3_march_kernel(const TV* __restrict__ 
         }
         __syncthreads();
         // y-window: kTX columns x (kTY / kKY) segments; lanes on consecutive x (coalesced)
-        {
-            const int tx = threadIdx.x % kTX, sy = (threadIdx.x / kTX) * kKY;
-            const int gx = x0 + tx;
-            TA s;
-            acc_zero(s);
+        const int tx = threadIdx.x % kTX, sy = (threadIdx.x / kTX) * kKY;
+        const int gx = x0 + tx;
+        TA s;
+        acc_zero(s);
 #pragma unroll
-            for (int j = 0; j <= 2 * R; ++j) acc_add(s, X[sy + j][tx]);
+        for (int j = 0; j <= 2 * R; ++j) acc_add(s, X[sy + j][tx]);
 #pragma unroll
-            for (int j = 0; j < kKY; ++j) {
-                if (j > 0) {
-                    acc_add(s, X[sy + j + 2 * R][tx]);
-                    acc_sub(s, X[sy + j - 1][tx]);
-                }
-                const int gy = y0 + sy + j;
-                if (gx < nx && gy < ny) put(ovol[(int64_t)z * plane + (int64_t)gy * nx + gx], s);
+        for (int j = 0; j < kKY; ++j) {
+            if (j > 0) {
+                acc_add(s, X[sy + j + 2 * R][tx]);
+                acc_sub(s, X[sy + j - 1][tx]);
             }
+            const int gy = y0 + sy + j;
+            if (gx < nx && gy < ny) put(ovol[(int64_t)z * plane + (int64_t)gy * nx + gx], s);
         }
         // (the next step's Z writes come after every thread passed the barrier above, i.e.
         //  after all x-window reads of Z; the next X writes follow its first barrier)
+    };
+    TA zs[NPT];
+    TV pa[NPT];
+    if constexpr (box3_ring<R, TV, NPT>()) {
+        // ring[j] holds slice z0 - R - 1 + j (mod W): the leaving slice of step z sits in slot
+        // (z - z0) % W, the slot the entering slice z + R then takes over
+        TV ring[W][NPT];
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) {
+            acc_zero(zs[k]);
+#pragma unroll
+            for (int j = 0; j < W; ++j) {  // the window of slice z0 - 1
+                ring[j][k] = load(z0 - R - 1 + j, k);
+                acc_add(zs[k], ring[j][k]);
+            }
+            pa[k] = load(z0 + R, k);
+        }
+        for (int zb = z0; zb < z1; zb += W) {
+#pragma unroll
+            for (int j = 0; j < W; ++j) {
+                const int z = zb + j;
+                if (z < z1) {  // uniform per workgroup
+#pragma unroll
+                    for (int k = 0; k < NPT; ++k) {
+                        acc_add(zs[k], pa[k]);
+                        acc_sub(zs[k], ring[j][k]);
+                        ring[j][k] = pa[k];
+                        if (ey_[k] >= 0) Z[ey_[k]][ex_[k]] = zs[k];
+                    }
+#pragma unroll
+                    for (int k = 0; k < NPT; ++k) pa[k] = load(z + 1 + R, k);
+                    xy_windows(z);
+                }
+            }
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) {  // window of slice z0 - 1
+            acc_zero(zs[k]);
+            for (int z = z0 - 1 - R; z <= z0 - 1 + R; ++z) acc_add(zs[k], load(z, k));
+        }
+        TV ps[NPT];
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) {
+            pa[k] = load(z0 + R, k);
+            ps[k] = load(z0 - R - 1, k);
+        }
+        for (int z = z0; z < z1; ++z) {
+#pragma unroll
+            for (int k = 0; k < NPT; ++k) {
+                acc_add(zs[k], pa[k]);
+                acc_sub(zs[k], ps[k]);
+                if (ey_[k] >= 0) Z[ey_[k]][ex_[k]] = zs[k];
+            }
+#pragma unroll
+            for (int k = 0; k < NPT; ++k) {  // next step's entering / leaving slices
+                pa[k] = load(z + 1 + R, k);
+                ps[k] = load(z - R, k);
+            }
+            xy_windows(z);
+        }
     }
 }
 
@@ -429,18 +491,22 @@ __device__ __forceinline__ void store_dtype(void* out, int dtype, int64_t i, flo
 
 // K3f: one workgroup marches one 64 x kTY xy tile of the OUTPUT box through a z segment of it, for
 // one output timepoint; the running z-window (f64 pair) covers the tile's R apron, whose loads
-// reach into the block's halo (zero outside the block: the clamped windows).
-// K3f: one workgroup marches one 64 x kTY xy tile of the OUTPUT box through a z segment of it, for
-// one output timepoint; the running z-window (f64 pair) covers the tile's R apron, whose loads
-// reach into the block's halo (zero outside the block: the clamped windows).
-template <int R>
-__global__ __launch_bounds__(kNT) void box3_final_kernel(const float2* __restrict__ TAB,
+// reach into the block's halo (zero outside the block: the clamped windows). The leaving slice
+// comes from a register ring when it fits (box3_ring), as in box3_march_kernel.
+// TYF: output tile height (kTY; 64 x 32 tiles measured 55.9 against 54.0 ms on the T share)
+template <int R, bool RING, int TYF>
+__global__ __launch_bounds__(RING ? kTX * TYF / 2 : kNT) void box3_final_kernel(
+    const float2* __restrict__ TAB,
                                                          const float* __restrict__ v,
                                                          void* __restrict__ out, int dtype_out,
                                                          NdGeom g, int zseg, int tiles_x,
                                                          int tiles_y, Str3 vs) {
-    constexpr int EX = kTX + 2 * R, EY = kTY + 2 * R, NE = EX * EY;
-    constexpr int NPT = (NE + kNT - 1) / kNT;
+    // RING: two outputs per thread in the y-window (512 threads for 64 x 16 tiles), so a thread
+    // owns half the apron points and its ring fits without cutting occupancy
+    constexpr int NT = RING ? kTX * TYF / 2 : kNT, KY = kTX * TYF / NT;
+    constexpr int EX = kTX + 2 * R, EY = TYF + 2 * R, NE = EX * EY;
+    constexpr int NPT = (NE + NT - 1) / NT;
+    constexpr int W = 2 * R + 1;
     // the running z-window is an f64 pair in registers (exact add / subtract); the x and y
     // windows of it go through LDS as f32 pairs (stage 2 is rounded to f32 anyway: half the LDS
     // bytes and f32 instead of f64 adds; the x / y sliding sums span kKX / kKY outputs only)
@@ -448,59 +514,41 @@ __global__ __launch_bounds__(kNT) void box3_final_kernel(const float2* __restric
     __shared__ float2 X[EY][kTX];
     const int T = (int)g.shape[0], nz = (int)g.shape[1], ny = (int)g.shape[2],
               nx = (int)g.shape[3];
-    const int ot = blockIdx.y;
+    int bx, ot;
+    xcd_block(bx, ot);
     const int t = ot + (int)g.out_start[0];
     const int ntile = tiles_x * tiles_y;
-    const int seg = blockIdx.x / ntile, tile = blockIdx.x % ntile;
+    const int seg = bx / ntile, tile = bx % ntile;
     const int ox0 = (int)g.out_start[3], oy0 = (int)g.out_start[2], oz0 = (int)g.out_start[1];
     const int ox1 = ox0 + (int)g.out_shape[3], oy1 = oy0 + (int)g.out_shape[2];
-    const int x0 = ox0 + (tile % tiles_x) * kTX, y0 = oy0 + (tile / tiles_x) * kTY;
+    const int x0 = ox0 + (tile % tiles_x) * kTX, y0 = oy0 + (tile / tiles_x) * TYF;
     const int z0 = oz0 + seg * zseg, z1 = min(z0 + zseg, oz0 + (int)g.out_shape[1]);
     const int64_t plane = (int64_t)ny * nx;
     const float2* vol = TAB + (int64_t)ot * nz * plane;
     const int ct = min(t + R, T - 1) - max(t - R, 0) + 1;
 
-    int64_t pidx[NPT];
-    int ey_[NPT], ex_[NPT];
+    // owned apron points: plane index (or -1) and Z offset (or -1). The ring variant needs every
+    // register it can get: 32-bit plane indices (the host checks ny * nx < 2^31)
+    using PI = std::conditional_t<RING, int, int64_t>;
+    PI pidx[NPT];
+    int zoff[NPT];
 #pragma unroll
     for (int k = 0; k < NPT; ++k) {
-        const int e = threadIdx.x + k * kNT;
+        const int e = threadIdx.x + k * NT;
         const int ey = e / EX, ex = e % EX;
         const int gy = y0 - R + ey, gx = x0 - R + ex;
-        ey_[k] = e < NE ? ey : -1;
-        ex_[k] = ex;
-        pidx[k] = (e < NE && gy >= 0 && gy < ny && gx >= 0 && gx < nx) ? (int64_t)gy * nx + gx : -1;
+        zoff[k] = e < NE ? e : -1;  // Z[ey][ex] == (&Z[0][0])[e]
+        pidx[k] = (e < NE && gy >= 0 && gy < ny && gx >= 0 && gx < nx) ? (PI)gy * nx + gx : (PI)-1;
     }
+    float2* const Zf = &Z[0][0];
     auto load = [&](int z, int k) -> float2 {
         return (pidx[k] >= 0 && z >= 0 && z < nz) ? vol[(int64_t)z * plane + pidx[k]]
                                                    : make_float2(0.f, 0.f);
     };
-    dd2 zs[NPT];
-#pragma unroll
-    for (int k = 0; k < NPT; ++k) {  // window of slice z0 - 1
-        acc_zero(zs[k]);
-        for (int z = z0 - 1 - R; z <= z0 - 1 + R; ++z) acc_add(zs[k], load(z, k));
-    }
-    float2 pa[NPT], ps[NPT];
-#pragma unroll
-    for (int k = 0; k < NPT; ++k) {
-        pa[k] = load(z0 + R, k);
-        ps[k] = load(z0 - R - 1, k);
-    }
-    for (int z = z0; z < z1; ++z) {
-#pragma unroll
-        for (int k = 0; k < NPT; ++k) {
-            acc_add(zs[k], pa[k]);
-            acc_sub(zs[k], ps[k]);
-            if (ey_[k] >= 0) Z[ey_[k]][ex_[k]] = make_float2((float)zs[k].x, (float)zs[k].y);
-        }
-#pragma unroll
-        for (int k = 0; k < NPT; ++k) {
-            pa[k] = load(z + 1 + R, k);
-            ps[k] = load(z - R, k);
-        }
+    // x / y windows of the Z slice of output slice z and the final stage
+    auto xy_final = [&](int z) {
         __syncthreads();
-        for (int it = threadIdx.x; it < EY * (kTX / kKX); it += kNT) {
+        for (int it = threadIdx.x; it < EY * (kTX / kKX); it += NT) {
             const int ey = it / (kTX / kKX), sx = (it % (kTX / kKX)) * kKX;
             float2 sacc = make_float2(0.f, 0.f);
 #pragma unroll
@@ -514,31 +562,88 @@ __global__ __launch_bounds__(kNT) void box3_final_kernel(const float2* __restric
             }
         }
         __syncthreads();
-        {
-            const int tx = threadIdx.x % kTX, sy = (threadIdx.x / kTX) * kKY;
-            const int gx = x0 + tx;
-            const int czx = ccount(z, nz, R) * ccount(gx, nx, R) * ct;
-            float2 sacc = make_float2(0.f, 0.f);
+        const int tx = threadIdx.x % kTX, sy = (threadIdx.x / kTX) * KY;
+        const int gx = x0 + tx;
+        const int czx = ccount(z, nz, R) * ccount(gx, nx, R) * ct;
+        float2 sacc = make_float2(0.f, 0.f);
 #pragma unroll
-            for (int j = 0; j <= 2 * R; ++j) acc_add(sacc, X[sy + j][tx]);
+        for (int j = 0; j <= 2 * R; ++j) acc_add(sacc, X[sy + j][tx]);
 #pragma unroll
-            for (int j = 0; j < kKY; ++j) {
-                if (j > 0) {
-                    acc_add(sacc, X[sy + j + 2 * R][tx]);
-                    acc_sub(sacc, X[sy + j - 1][tx]);
-                }
-                const int gy = y0 + sy + j;
-                if (gx < ox1 && gy < oy1) {
-                    const float cnt = (float)(czx * ccount(gy, ny, R));
-                    const float ma = (float)sacc.x / cnt, mb = (float)sacc.y / cnt;
-                    const float vv = v[t * vs.t + (int64_t)z * vs.z + (int64_t)gy * vs.y + gx];
-                    const float o = __fadd_rn(__fmul_rn(vv, ma), mb);  // v *= ma; v += mb
-                    store_dtype(out, dtype_out,
-                                ot * g.out_strides[0] + (z - oz0) * g.out_strides[1] +
-                                    (gy - oy0) * g.out_strides[2] + (gx - ox0) * g.out_strides[3],
-                                o);
+        for (int j = 0; j < KY; ++j) {
+            if (j > 0) {
+                acc_add(sacc, X[sy + j + 2 * R][tx]);
+                acc_sub(sacc, X[sy + j - 1][tx]);
+            }
+            const int gy = y0 + sy + j;
+            if (gx < ox1 && gy < oy1) {
+                const float cnt = (float)(czx * ccount(gy, ny, R));
+                const float ma = (float)sacc.x / cnt, mb = (float)sacc.y / cnt;
+                const float vv = v[t * vs.t + (int64_t)z * vs.z + (int64_t)gy * vs.y + gx];
+                const float o = __fadd_rn(__fmul_rn(vv, ma), mb);  // v *= ma; v += mb
+                store_dtype(out, dtype_out,
+                            ot * g.out_strides[0] + (z - oz0) * g.out_strides[1] +
+                                (gy - oy0) * g.out_strides[2] + (gx - ox0) * g.out_strides[3],
+                            o);
+            }
+        }
+    };
+    dd2 zs[NPT];
+    float2 pa[NPT];
+    if constexpr (RING && box3_ring<R, float2, NPT>()) {
+        float2 ring[W][NPT];  // slot (z - z0) % W: the leaving slice of step z (box3_march_kernel)
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) {
+            acc_zero(zs[k]);
+#pragma unroll
+            for (int j = 0; j < W; ++j) {
+                ring[j][k] = load(z0 - R - 1 + j, k);
+                acc_add(zs[k], ring[j][k]);
+            }
+            pa[k] = load(z0 + R, k);
+        }
+        for (int zb = z0; zb < z1; zb += W) {
+#pragma unroll
+            for (int j = 0; j < W; ++j) {
+                const int z = zb + j;
+                if (z < z1) {  // uniform per workgroup
+#pragma unroll
+                    for (int k = 0; k < NPT; ++k) {
+                        acc_add(zs[k], pa[k]);
+                        acc_sub(zs[k], ring[j][k]);
+                        ring[j][k] = pa[k];
+                        if (zoff[k] >= 0) Zf[zoff[k]] = make_float2((float)zs[k].x, (float)zs[k].y);
+                    }
+#pragma unroll
+                    for (int k = 0; k < NPT; ++k) pa[k] = load(z + 1 + R, k);
+                    xy_final(z);
                 }
             }
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) {  // window of slice z0 - 1
+            acc_zero(zs[k]);
+            for (int z = z0 - 1 - R; z <= z0 - 1 + R; ++z) acc_add(zs[k], load(z, k));
+        }
+        float2 ps[NPT];
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) {
+            pa[k] = load(z0 + R, k);
+            ps[k] = load(z0 - R - 1, k);
+        }
+        for (int z = z0; z < z1; ++z) {
+#pragma unroll
+            for (int k = 0; k < NPT; ++k) {
+                acc_add(zs[k], pa[k]);
+                acc_sub(zs[k], ps[k]);
+                if (zoff[k] >= 0) Zf[zoff[k]] = make_float2((float)zs[k].x, (float)zs[k].y);
+            }
+#pragma unroll
+            for (int k = 0; k < NPT; ++k) {
+                pa[k] = load(z + 1 + R, k);
+                ps[k] = load(z - R, k);
+            }
+            xy_final(z);
         }
     }
 }
@@ -584,6 +689,16 @@ static bool g4_legacy() {
     static const bool on = [] {
         const char* e = getenv("ZT_G4_LEGACY");
         return e && e[0] == '1';
+    }();
+    return on;
+}
+
+// ZT_G4_FINAL_RING=0: box3_final_kernel re-reads the leaving slice instead of holding the z-window
+// ring in registers (A/B runs)
+static bool g4_final_ring() {
+    static const bool on = [] {
+        const char* e = getenv("ZT_G4_FINAL_RING");
+        return !(e && e[0] == '0');
     }();
     return on;
 }
@@ -654,6 +769,7 @@ hipError_t launch_guided4d(const void* in, int dtype_in, void* out, int dtype_ou
         else return hipErrorInvalidValue;
         if ((e = hipGetLastError()) != hipSuccess) return e;
         const int64_t onx = g.out_shape[3], ony = g.out_shape[2], onz = g.out_shape[1];
+        const bool ring = g4_final_ring() && (int64_t)ny * nx < ((int64_t)1 << 31);
         const int tiles_x = (int)((onx + kTX - 1) / kTX), tiles_y = (int)((ony + kTY - 1) / kTY);
         const int64_t tiles = (int64_t)tiles_x * tiles_y;
         int nseg = (int)std::max<int64_t>(
@@ -667,8 +783,12 @@ hipError_t launch_guided4d(const void* in, int dtype_in, void* out, int dtype_ou
         switch (radius) {
 #define ZT_G4_K3F(RR)                                                                             \
     case RR:                                                                                      \
-        hipLaunchKernelGGL((box3_final_kernel<RR>), fg, dim3(kNT), 0, s, TAB, v, out, dtype_out,   \
-                           g, zseg, tiles_x, tiles_y, vs);                                        \
+        if (ring)                                                                                 \
+            hipLaunchKernelGGL((box3_final_kernel<RR, true, kTY>), fg, dim3(kTX * kTY / 2), 0, s, TAB,\
+                               v, out, dtype_out, g, zseg, tiles_x, tiles_y, vs);                 \
+        else                                                                                      \
+            hipLaunchKernelGGL((box3_final_kernel<RR, false, kTY>), fg, dim3(kNT), 0, s, TAB, v,   \
+                               out, dtype_out, g, zseg, tiles_x, tiles_y, vs);                    \
         break;
             ZT_G4_K3F(1) ZT_G4_K3F(2) ZT_G4_K3F(3) ZT_G4_K3F(4) ZT_G4_K3F(5) ZT_G4_K3F(6)
 #undef ZT_G4_K3F
