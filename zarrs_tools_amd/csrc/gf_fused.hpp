@@ -28,6 +28,9 @@
 #ifndef GF_HX_B128
 #define GF_HX_B128 1  // 16-byte Hx writes for even R (fewer LDS bank conflicts: -2% at r=4)
 #endif
+#ifndef GF_P1RING_MAXR
+#define GF_P1RING_MAXR 2  // stage-1 z-window ring in registers up to this radius (see GFConfig)
+#endif
 #ifndef GF_K3
 #define GF_K3 4  // P3 outputs per thread (column segment of the f64 y-window)
 #endif
@@ -524,6 +527,10 @@ struct GFConfig {
     // single pass: P12 rows on the top waves (P4 works on the bottom ones)
     static constexpr int W12 = NQP1 == 1 ? NWAVE - (E2Y + RPW - 1) / RPW : 0;
     static constexpr int NB = (R + EPL - 1) / EPL;         // neighbour lanes on each side
+    // P1 ring: the last W entering stage-1 quads of a lane held in registers, so the leaving
+    // slice of the running z-window is never re-read (W * NQP1 * 4 VGPRs: 20 at r = 2, where the
+    // 64 x 32 tile leaves ~40 free; at r = 4 the kernel has 5 to spare, so it re-reads)
+    static constexpr bool P1RING = R <= GF_P1RING_MAXR;
     static constexpr int NQ5 = TX / 4 * TY;                  // output tile quads
     static constexpr int W3 = W * W * W;                     // interior window count
     static constexpr int al(int b) { return (b + 255) / 256 * 256; }
@@ -678,7 +685,27 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     // Running z-window: seed Zv(zc_begin - 1) = sum of v over [zc_begin-1-R, zc_begin-1+R]
     // clamped to [0, nz); every later step adds the entering and subtracts the leaving slice
     // (both 0 outside the domain), so the window stays exact through out-of-domain steps.
-    {
+    // With the P1 ring, P12(c) (entering slice c+R, leaving c-R-1) uses slot
+    // (c - zc_begin + W - 1) % W: the prologue's P12(zc_begin) slot W-1, the march's P12(i+1) of
+    // unrolled step k slot k. Seed slice zc_begin-1-R+j entered as P12(zc_begin-1-2R+j): slot
+    // (j + W - 1) % W.
+    SI ring1[C::P1RING ? W : 1][C::NQP1][EPL];
+    if constexpr (C::P1RING) {
+        static_for<0, W>([&](auto jc) {
+            constexpr int j = decltype(jc)::value;
+            const rsrc_t rs = slice_rsrc(zc_begin - 1 - R + j);  // 0 outside [zlo, zhi)
+#pragma unroll
+            for (int k = 0; k < C::NQP1; ++k) {
+                SI v[4];
+                load_quad(rs, q1off[k], q1mask[k], v);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    ring1[(j + W - 1) % W][k][e] = v[e];
+                    zv[k][e] += (SA)v[e];
+                }
+            }
+        });
+    } else {
         const int za = max(zc_begin - 1 - R, 0), zb_ = min(zc_begin - 1 + R, nz - 1);
         for (int z = za; z <= zb_; ++z) {
             const rsrc_t rs = slice_rsrc(z);
@@ -711,18 +738,19 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
         for (int k = 0; k < C::NQP1; ++k) {
             SI a4[4], s4[4];
             load_quad(ra, q1off[k], q1mask[k], a4);
-            load_quad(rs, q1off[k], q1mask[k], s4);
+            if constexpr (!C::P1RING) load_quad(rs, q1off[k], q1mask[k], s4);
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 pa[k][e] = a4[e];
-                ps[k][e] = s4[e];
+                if constexpr (!C::P1RING) ps[k][e] = s4[e];
             }
         }
     };
     // P12: z-window of v (f64, running) and its x-window sums on the E2 apron -> Hx. The x
     // neighbours come from the adjacent lanes' quads by DPP wave shifts (whole rows per wave),
     // so the z-window never goes through LDS.
-    auto do_p12 = [&](int tid) {
+    auto do_p12 = [&](int tid, auto slotc) {
+        constexpr int sl = decltype(slotc)::value;  // P1 ring slot of this step
 #pragma unroll
         for (int k = 0; k < C::NQP1; ++k) {
             int row, cq;
@@ -730,7 +758,12 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
 #pragma unroll
             for (int e = 0; e < EPL; ++e) {
                 zv[k][e] = zv[k][e] + (SA)pa[k][e];  // entering slice (0 outside the domain)
-                zv[k][e] = zv[k][e] - (SA)ps[k][e];  // leaving slice (0 outside the domain)
+                if constexpr (C::P1RING) {
+                    zv[k][e] = zv[k][e] - (SA)ring1[sl][k][e];  // leaving slice, from the ring
+                    ring1[sl][k][e] = pa[k][e];
+                } else {
+                    zv[k][e] = zv[k][e] - (SA)ps[k][e];  // leaving slice (0 outside the domain)
+                }
             }
             constexpr int NB = C::NB;
             SA win[EPL * (2 * NB + 1)];  // lane items cq-NB .. cq+NB
@@ -1000,7 +1033,7 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     // ---- prologue: stage 1 of the first slice up to Hx; prefetch step 1 ---------------------
     load_p1(slice_rsrc(zc_begin + R), slice_rsrc(zc_begin - R - 1));
     load_p3v(slice_rsrc(zc_begin));
-    do_p12(tid0);
+    do_p12(tid0, std::integral_constant<int, W - 1>{});
     load_p1(slice_rsrc(zc_begin + 1 + R), slice_rsrc(zc_begin - R));
     lds_barrier();
 
@@ -1053,7 +1086,7 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
             load_p3v(rs_in(ob + (int64_t)R * sstride, zb + R));  // P3 slice i+1
             load_p5v(rs_in(ob - sstride, zb - 1));                // P5 slice i-R
             if constexpr (C::ORDER & 2) do_p4(tid);
-            do_p12(tid);
+            do_p12(tid, kc);
             load_p1(rs_in(ob + off_a, zb + 2 * R + 1), r_b);
             if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(1);
             if constexpr (!(C::ORDER & 2)) do_p4(tid);
