@@ -61,7 +61,8 @@ def main():
             wall = time.perf_counter() - t0
             res[mode] = {"wall_s": round(wall, 3), "levels": r["levels"],
                          "input_gvox_per_s": round(a.size ** 3 / wall / 1e9, 3),
-                         "level_s": [round(st["wall_s"], 3) for st in r["stats"]]}
+                         "level_s": [round(st["wall_s"], 3) for st in r["stats"]],
+                         "phases": r.get("phases", {})}
             oct_st = [st for st in r["stats"] if "per_rank" in st]
             if oct_st:  # the octant workers' own phases (box read, device pyramid, writes)
                 res[mode]["octant_ranks"] = [

@@ -310,14 +310,36 @@ def prepare_octant_levels(out_root: str, level_shapes, local_levels: int, src0=N
         _hold_metadata(dst)
 
 
+def _octant_warmup(device: int) -> float:
+    """Run first on each pre-spawned octant worker (octant_pool): import torch and this package
+    and create the device's context while the parent still prepares the levels. The spawned
+    interpreter's start-up is most of a small rank's time."""
+    import torch
+    from . import filter as _F  # noqa: F401  (loads the HIP library)
+    if torch.cuda.is_available() and device < torch.cuda.device_count():
+        torch.empty(1, device=f"cuda:{device}")
+    return time.time()
+
+
+def octant_pool(gpus: int, devices):
+    """The spawned process pool of run_octants, started early with a warm-up task per process,
+    before this process initialises any device (spawn, not fork)."""
+    import multiprocessing as mp
+    from concurrent.futures import ProcessPoolExecutor
+    ex = ProcessPoolExecutor(gpus, mp_context=mp.get_context("spawn"))
+    for d in list(devices)[:gpus]:
+        ex.submit(_octant_warmup, d)
+    return ex
+
+
 def run_octants(out_root: str, shape0, factor, levels, discrete: bool, gpus: int, devices=None,
-                nthreads: int = 0, log=print, compute=None, src0=None):
+                nthreads: int = 0, log=print, compute=None, src0=None, pool=None):
     """Levels 1..L of the pyramid over `gpus` processes, one per GPU, each owning a factor^L-
     aligned box of level 0 (shard.octant_assignment; no exchange between processes). The level
     arrays 1..L must exist with pending metadata; chunks crossing box boundaries are assembled
-    on the host (shard.assemble_chunk) and written by this (parent) process. Returns (L, stats)."""
-    import multiprocessing as mp
-    from concurrent.futures import ProcessPoolExecutor
+    on the host (shard.assemble_chunk) and written by this (parent) process. `pool`: a process
+    pool from octant_pool (the caller shuts it down), else one is spawned here. Returns (L,
+    stats)."""
     from . import shard
     assigns = [shard.octant_assignment(g, gpus, shape0, factor, levels) for g in range(gpus)]
     L = assigns[0].local_levels
@@ -327,12 +349,16 @@ def run_octants(out_root: str, shape0, factor, levels, discrete: bool, gpus: int
     envs = [{"ZT_STORE_HOST_MEMORY": str(host_share)} for _ in range(gpus)]
     scratch = tempfile.mkdtemp(prefix=".zt_octants_", dir=out_root)
     t0 = time.perf_counter()
+    ex = pool if pool is not None else octant_pool(gpus, [])
     try:
-        with ProcessPoolExecutor(gpus, mp_context=mp.get_context("spawn")) as ex:
+        try:
             futs = [ex.submit(_octant_worker, out_root, assigns[g], list(factor), discrete,
                               devices[g], per, scratch, envs[g], compute, src0)
                     for g in range(gpus) if assigns[g].coord is not None]
             parts = [f.result() for f in futs]
+        finally:
+            if pool is None:
+                ex.shutdown()
         t1 = time.perf_counter()
         # host assembly of the chunks that cross box boundaries
         by_chunk: dict = {}
@@ -398,6 +424,23 @@ def run(input_path, output_path, factor=None, max_levels: int = 10, discrete: bo
     if group_attributes:
         group_attrs.update(json.loads(group_attributes) if isinstance(group_attributes, str)
                            else group_attributes)
+    # octant workers (gpus > 1, no Gaussian) spawned now, so their start-up overlaps this
+    # process's preparation; unused (and shut down) if the levels do not take the octant path
+    pool = octant_pool(gpus, list(gpu_devices or range(gpus))) if gpus > 1 and gauss is None \
+        else None
+    try:
+        return _run(input_path, output_path, info, nd, factor, max_levels, discrete, name, exists,
+                    device, nthreads, gauss, physical_size, physical_units, group_attrs, reencoding,
+                    log, device_resident, chunk_limit, gpus, gpu_devices, pool, t0)
+    finally:
+        if pool is not None:
+            pool.shutdown()
+
+
+def _run(input_path, output_path, info, nd, factor, max_levels, discrete, name, exists, device,
+         nthreads, gauss, physical_size, physical_units, group_attrs, reencoding, log,
+         device_resident, chunk_limit, gpus, gpu_devices, pool, t0) -> dict:
+    """The body of run() once its arguments are checked (`pool`: octant_pool or None)."""
     if os.path.exists(output_path):
         if exists == "exit":
             raise _abi.FilterError(_abi.ERR_OTHER, "Output exists, exiting")
@@ -420,6 +463,7 @@ def run(input_path, output_path, factor=None, max_levels: int = 10, discrete: bo
                  and _device_pyramid_fits(info0, gauss, device))
     cur = None  # the previous level in HBM (device-resident pyramid)
     copy_thread, copy_err = None, []
+    phases = {}  # wall-clock phases of this call (seconds since its start), for the e2e tools
     if reencoding:
         _reencode_level0(input_path, lvl0, reencoding, nthreads, log, device)
     else:
@@ -431,10 +475,12 @@ def run(input_path, output_path, factor=None, max_levels: int = 10, discrete: bo
         import threading
 
         def _copy():
+            phases["copy_start"] = time.perf_counter() - t0
             try:
                 shutil.copytree(input_path, lvl0)
             except BaseException as e:  # re-raised below
                 copy_err.append(e)
+            phases["copy_end"] = time.perf_counter() - t0
         copy_thread = threading.Thread(target=_copy)
         copy_thread.start()
         if on_device:
@@ -454,15 +500,18 @@ def run(input_path, output_path, factor=None, max_levels: int = 10, discrete: bo
         # every distinct device must hold its processes' boxes (each with its own count)
         fits = all(_device_pyramid_fits(box_info, None, d, sharing=devices.count(d),
                                         host_share=gpus) for d in sorted(set(devices)))
+        phases["octant_checks_done"] = time.perf_counter() - t0
         if big.local_levels > 0 and fits:
             prepare_octant_levels(output_path, level_shapes, big.local_levels, src0)
             octants_done, st_oct = run_octants(output_path, list(info.shape), factor,
                                                len(level_shapes), discrete, gpus, devices,
-                                               nthreads, log, src0=src0)
+                                               nthreads, log, src0=src0, pool=pool)
             st_oct["levels"] = octants_done
             stats.append(st_oct)
+            phases["octants_done"] = time.perf_counter() - t0
     if copy_thread is not None:
         copy_thread.join()
+        phases["copy_joined"] = time.perf_counter() - t0
         if copy_err:
             raise copy_err[0]
         log(f"0: copy {input_path} -> {lvl0} ({info.data_type} {list(info.shape)})")
@@ -577,7 +626,9 @@ def run(input_path, output_path, factor=None, max_levels: int = 10, discrete: bo
     with open(os.path.join(output_path, "zarr.json"), "w") as f:
         json.dump(group, f, indent=2)
     log(f"Output {output_path} in {time.perf_counter() - t0:.2f}s")
-    return {"levels": len(level_shapes), "stats": stats}
+    phases["end"] = time.perf_counter() - t0
+    return {"levels": len(level_shapes), "stats": stats,
+            "phases": {k: round(v, 3) for k, v in phases.items()}}
 
 
 def main(argv=None) -> int:
