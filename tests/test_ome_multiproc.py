@@ -59,3 +59,22 @@ def test_box_chunks_inner_box_and_touched_chunks():
     lo, hi, i0, i1 = ZO._box_chunks((8, 0), (24, 40), (16, 16), (32, 40))
     assert (lo, hi) == ([0, 0], [2, 3])
     assert (i0, i1) == ([16, 0], [32, 40])  # the array end counts as a chunk boundary
+
+
+@pytest.mark.parametrize("nthreads", [1, 8])
+def test_copy_tree_equals_copytree(tmp_path, nthreads):
+    # level 0's threaded copy (zarrs_ome.copy_tree) gives the tree shutil.copytree gives
+    src = tmp_path / "in.zarr"
+    S.create_array(src, "uint16", (40, 40, 40), (8, 8, 8))
+    S.write_array(src, np.arange(40 ** 3, dtype=np.uint16).reshape(40, 40, 40), (0, 0, 0))
+    ZO.copy_tree(str(src), str(tmp_path / "a"), nthreads)
+    shutil.copytree(src, tmp_path / "b")
+    walk = lambda r: sorted((os.path.relpath(d, r), sorted(f)) for d, _, f in os.walk(r))
+    assert walk(tmp_path / "a") == walk(tmp_path / "b")
+    for d, _, files in os.walk(tmp_path / "b"):
+        for f in files:
+            rel = os.path.relpath(os.path.join(d, f), tmp_path / "b")
+            assert open(tmp_path / "a" / rel, "rb").read() == open(tmp_path / "b" / rel, "rb").read()
+    np.testing.assert_array_equal(S.read_array(tmp_path / "a"), S.read_array(src))
+    with pytest.raises(FileExistsError):
+        ZO.copy_tree(str(src), str(tmp_path / "a"), nthreads)
