@@ -73,6 +73,21 @@ struct Str3 {
     int64_t t, z, y;
 };
 
+#ifndef G4_LDS_BARRIER
+#define G4_LDS_BARRIER 0
+#endif
+// The box3 marches' step barrier. __syncthreads() also waits for every global load in flight,
+// i.e. for the next step's prefetched entering slice; G4_LDS_BARRIER=1 waits for LDS only, so the
+// prefetch stays in flight across the barrier (the compiler still waits for it at its first use).
+// Measured slower on the T share (57.1-57.2 against 55.2-55.4 ms, profiles/r04_ldsbar_ab.jsonl).
+__device__ __forceinline__ void box3_barrier() {
+#if G4_LDS_BARRIER
+    __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#else
+    __syncthreads();
+#endif
+}
+
 // XCD-aware block order. Consecutive linear block ids are dispatched round-robin over the 8 XCDs
 // (each with its own L2); give each XCD a contiguous run of (tile, timepoint) ids instead, so the
 // workgroups resident on one XCD march neighbouring tiles whose aprons share that XCD's L2 lines.
@@ -135,7 +150,7 @@ __global__ __launch_bounds__(kNT) void box3_march_kernel(const TV* __restrict__ 
     };
     // x- and y-window sums of the Z slice of output slice z (the caller filled Z)
     auto xy_windows = [&](int z) {
-        __syncthreads();
+        box3_barrier();
         // x-window: EY rows x (kTX / kKX) segments of kKX outputs
         for (int it = threadIdx.x; it < EY * (kTX / kKX); it += kNT) {
             const int ey = it / (kTX / kKX), sx = (it % (kTX / kKX)) * kKX;
@@ -151,7 +166,7 @@ __global__ __launch_bounds__(kNT) void box3_march_kernel(const TV* __restrict__ 
                 X[ey][sx + j] = s;
             }
         }
-        __syncthreads();
+        box3_barrier();
         // y-window: kTX columns x (kTY / kKY) segments; lanes on consecutive x (coalesced)
         const int tx = threadIdx.x % kTX, sy = (threadIdx.x / kTX) * kKY;
         const int gx = x0 + tx;
@@ -547,7 +562,7 @@ __global__ __launch_bounds__(RING ? kTX * TYF / 2 : kNT) void box3_final_kernel(
     };
     // x / y windows of the Z slice of output slice z and the final stage
     auto xy_final = [&](int z) {
-        __syncthreads();
+        box3_barrier();
         for (int it = threadIdx.x; it < EY * (kTX / kKX); it += NT) {
             const int ey = it / (kTX / kKX), sx = (it % (kTX / kKX)) * kKX;
             float2 sacc = make_float2(0.f, 0.f);
@@ -561,7 +576,7 @@ __global__ __launch_bounds__(RING ? kTX * TYF / 2 : kNT) void box3_final_kernel(
                 X[ey][sx + j] = sacc;
             }
         }
-        __syncthreads();
+        box3_barrier();
         const int tx = threadIdx.x % kTX, sy = (threadIdx.x / kTX) * KY;
         const int gx = x0 + tx;
         const int czx = ccount(z, nz, R) * ccount(gx, nx, R) * ct;
