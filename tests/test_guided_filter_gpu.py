@@ -306,10 +306,23 @@ def test_guided4d_per_chunk_and_small_eps(r):
     ((12, 8, 9, 30), (4, 4, 9, 15), 1),      # TMAX = 16
 ])
 def test_guided4d_long_series_small_eps(shape, chunk, r):
-    """The four-kernel 4-D path for blocks of 5-32 timepoints (sliding t-windows, stage 2 as box3
+    """The three-kernel 4-D path for blocks of 5-32 timepoints (sliding t-windows, stage 2 as box3
     of the t-window sums with the final stage in the box3 march): whole box and per chunk equal
     the oracle at eps = 0.5 (exact stage 1)."""
     rng = np.random.default_rng(sum(shape) + r)
+    v = (rng.random(shape, dtype=np.float32) * 300).astype(np.float32)
+    ref = O.guided_filter_apply(v, chunk, 0.5, r, nthreads=8)
+    assert rel_err(gpu_apply(v, "float32", "float32", chunk, 0.5, r), ref) <= FLOAT_TOL
+    assert rel_err(gpu_apply_chunked(v, "float32", "float32", chunk, 0.5, r), ref) <= FLOAT_TOL
+
+
+@pytest.mark.parametrize("r", [1, 2, 3])
+def test_guided4d_z_ring_many_steps(r):
+    """The box3 marches' z-window register ring (box3_ring: the leaving slice from registers,
+    the march unrolled by 2r + 1) over a z extent of several ring turns that is no multiple of
+    2r + 1, with a z segment start inside the array (output box), against the oracle."""
+    rng = np.random.default_rng(100 + r)
+    shape, chunk = (6, 37, 20, 70), (3, 8, 10, 35)
     v = (rng.random(shape, dtype=np.float32) * 300).astype(np.float32)
     ref = O.guided_filter_apply(v, chunk, 0.5, r, nthreads=8)
     assert rel_err(gpu_apply(v, "float32", "float32", chunk, 0.5, r), ref) <= FLOAT_TOL
