@@ -133,6 +133,9 @@ def test_ome_cli_surface_and_helpers():
                                       "-s", "64,64,64", "-c", "32,32,32"])
     assert a.factor == [2, 2, 1] and a.physical_size == [0.5, 0.5, 1.0]
     assert a.exists == "overwrite" and a.shard_shape == [64, 64, 64]
+    assert a.gpu_devices is None
+    b = ZO.build_parser().parse_args(["i", "o", "--gpus", "2", "--gpu-devices", "0,0"])
+    assert b.gpus == 2 and b.gpu_devices == [0, 0]
     # units_to_axis (zarrs_ome.rs:390-432)
     assert ZO.axis_of("z", "micrometer") == {"name": "z", "type": "space", "unit": "micrometer"}
     assert ZO.axis_of("t", "second") == {"name": "t", "type": "time", "unit": "second"}

@@ -25,6 +25,9 @@ def main():
     ap.add_argument("--gpus", type=int, nargs="*", default=[],
                     help="also run zarrs_ome --gpus N for each N, every process on device 0 "
                          "(a one-GPU rehearsal of the octant split)")
+    ap.add_argument("--cli", action="store_true",
+                    help="also time each mode as a fresh `python -m zarrs_tools_amd.zarrs_ome` "
+                         "process (interpreter start-up and imports included, as a user sees it)")
     a = ap.parse_args()
     import numpy as np
     from oracle import oracle as O
@@ -72,6 +75,20 @@ def main():
                 got = S.read_array(os.path.join(out, str(lvl)), (0, 0, 0), want.shape)
                 ok = ok and bool(np.array_equal(got, want))
             shutil.rmtree(out, ignore_errors=True)  # (disk: one output at a time)
+            if a.cli:
+                import subprocess
+                cmd = [sys.executable, "-m", "zarrs_tools_amd.zarrs_ome", pin, out,
+                       "--max-levels", str(a.levels)]
+                if not dev:
+                    cmd.append("--no-device-resident")
+                if g > 1:
+                    cmd += ["--gpus", str(g), "--gpu-devices", ",".join(["0"] * g)]
+                t0 = time.perf_counter()
+                subprocess.run(cmd, check=True, cwd=ROOT, stdout=subprocess.DEVNULL)
+                res[mode]["cli_wall_s"] = round(time.perf_counter() - t0, 3)
+                got = S.read_array(os.path.join(out, "1"), (0, 0, 0), refs[0].shape)
+                ok = ok and bool(np.array_equal(got, refs[0]))
+                shutil.rmtree(out, ignore_errors=True)
         res["parity"] = {"bit_exact_corner_blocks": ok}
         print(json.dumps(res), flush=True)
     finally:

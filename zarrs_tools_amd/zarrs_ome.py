@@ -88,6 +88,9 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--gpus", type=int, default=1,
                     help="one process per GPU: octant-owned levels (mean / mode), or every "
                          "level split by output chunk rows (--gaussian-sigma)")
+    ap.add_argument("--gpu-devices", default=None, type=lambda s: [int(v) for v in s.split(",")],
+                    help="with --gpus N: process g runs on device LIST[g] (default 0..N-1; "
+                         "e.g. 0,0 rehearses a 2-GPU run on one device)")
     ap.add_argument("--no-device-resident", action="store_true",
                     help="read every level back from the store (the reference's loop)")
     _add_reencode_args(ap)  # adds --chunk-limit too
@@ -663,7 +666,7 @@ def main(argv=None) -> int:
             0, a.gaussian_sigma, a.gaussian_kernel_half_size,
             a.physical_size, a.physical_units, a.group_attributes, enc,
             device_resident=not a.no_device_resident, chunk_limit=a.filter_chunk_limit or 0,
-            gpus=a.gpus)
+            gpus=a.gpus, gpu_devices=a.gpu_devices)
     except _abi.FilterError as e:
         print(f"Error: {e}", file=sys.stderr)
         return 1
