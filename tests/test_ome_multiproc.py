@@ -23,8 +23,8 @@ def _level_u16_2x(x):
     return O.downsample(np.asarray(x), "uint16", (2, 2, 2), "uint16")
 
 
-@pytest.mark.parametrize("world", [2, 3, 4])
-def test_octant_processes_assemble_the_global_pyramid(tmp_path, world):
+@pytest.mark.parametrize("world,prespawn", [(2, False), (3, False), (4, False), (2, True)])
+def test_octant_processes_assemble_the_global_pyramid(tmp_path, world, prespawn):
     shape, chunk, factor = (64, 48, 80), (16, 16, 16), (2, 2, 2)
     u = O.synth_u16(shape)
     S.create_array(tmp_path / "in.zarr", "uint16", shape, chunk)
@@ -36,9 +36,15 @@ def test_octant_processes_assemble_the_global_pyramid(tmp_path, world):
     L = shard.octant_assignment(0, world, shape, factor, len(level_shapes)).local_levels
     assert L >= 2
     ZO.prepare_octant_levels(str(root), level_shapes, L)
-    done, st = ZO.run_octants(str(root), shape, factor, len(level_shapes), False, world,
-                              devices=[0] * world, log=lambda *a: None,
-                              compute=_level_u16_2x)
+    # prespawn: the pool zarrs_ome.run starts first (octant_pool, one warm-up task per process)
+    pool = ZO.octant_pool(world, [0] * world) if prespawn else None
+    try:
+        done, st = ZO.run_octants(str(root), shape, factor, len(level_shapes), False, world,
+                                  devices=[0] * world, log=lambda *a: None,
+                                  compute=_level_u16_2x, pool=pool)
+    finally:
+        if pool is not None:
+            pool.shutdown()
     assert done == L
     assert st["assembled_chunks"] > 0  # the upper levels cross box boundaries
     want = u
