@@ -461,7 +461,7 @@ def run(input_path, output_path, factor=None, max_levels: int = 10, discrete: bo
         if pool is not None:
             # every task is done here; the workers' exit (device teardown, ~0.8 s) need not hold
             # up the caller
-            pool.shutdown(wait=False)
+            pool.shutdown(wait=False, cancel_futures=True)
 
 
 def _run(input_path, output_path, info, nd, factor, max_levels, discrete, name, exists, device,
