@@ -317,6 +317,11 @@ def main():
                      "kernel_ms": round(kern_ms, 4),
                      "algorithmic_bytes_per_launch": voxels_rank * ALGO_BYTES_PER_VOXEL},
     }
+    if traffic is not None:
+        # the HBM bytes the kernel actually moves (PMC), per second of its launch: how close the
+        # access pattern runs to the memory system's rate, next to the algorithmic `achieved`
+        res["roofline"]["traffic_gbs"] = round(traffic / (kern_ms / 1000.0) / 1e9, 1)
+        res["roofline"]["traffic_frac"] = round(res["roofline"]["traffic_gbs"] / HBM_PEAK_GBS, 4)
     if share is not None:
         res["metric"] += f", rank {share[0]}'s share of a {share[1]}-GPU split (1-GPU proxy)"
         res["config"]["parallelism"] = f"share {share[0]}/{share[1]} on one GPU"
