@@ -52,6 +52,10 @@
 #ifndef SK_NOSTORE
 #define SK_NOSTORE 0  // 1: no output stores (the loads still feed an opaque never-taken store)
 #endif
+#ifndef SK_RINGBUF
+#define SK_RINGBUF 0  // 1: the leaving slice from a per-workgroup ring of the entering quads in global
+                      // memory (16 B per lane per slot, coalesced), written as they enter
+#endif
 #ifndef SK_TX
 #define SK_TX 64
 #endif
@@ -100,7 +104,7 @@ __device__ __forceinline__ int apron_off(int q, int x0, int y0, int n) {
 
 __global__ __launch_bounds__(NT) void skeleton_kernel(const float* __restrict__ in,
                                                       float* __restrict__ out, int n, int zseg,
-                                                      float* dummy) {
+                                                      float* dummy, float4* ringbuf) {
     extern __shared__ float sk_lds[];  // occupancy only (argv[2]); never touched
     const int nwg = gridDim.x, b = blockIdx.x;
     const int lid = (nwg % 8 == 0) ? (b % 8) * (nwg / 8) + b / 8 : b;
@@ -141,11 +145,17 @@ __global__ __launch_bounds__(NT) void skeleton_kernel(const float* __restrict__ 
     struct Step {
         float4 e[K1], l[K1], c[K3], v;
     };
+    constexpr int WR = 2 * R + 1;  // ring slots (the leaving slice entered WR steps earlier)
+    float4* const myring = ringbuf + (long)b * WR * K1 * NT;
+    auto rslot = [&](int zc) { return ((zc % WR) + WR) % WR; };
     auto load = [&](int zc, Step& s) {
 #pragma unroll
         for (int k = 0; k < K1; ++k) {
             s.e[k] = ld(in, slice, n, zc + R, o1[k]);
-            s.l[k] = ld(in, slice, n, zc + R - SK_LDIST, o1l[k]);
+            if (SK_RINGBUF)
+                s.l[k] = myring[(rslot(zc) * K1 + k) * NT + tid];
+            else
+                s.l[k] = ld(in, slice, n, zc + R - SK_LDIST, o1l[k]);
         }
 #pragma unroll
         for (int k = 0; k < K3; ++k) s.c[k] = ld(in, slice, n, zc, o3l[k]);
@@ -154,6 +164,10 @@ __global__ __launch_bounds__(NT) void skeleton_kernel(const float* __restrict__ 
     auto step = [&](int zc, const Step& s) {
 #pragma unroll
         for (int k = 0; k < K1; ++k) { add(s.e[k], 1.f); add(s.l[k], -1.f); }
+        if (SK_RINGBUF) {
+#pragma unroll
+            for (int k = 0; k < K1; ++k) myring[(rslot(zc) * K1 + k) * NT + tid] = s.e[k];
+        }
 #pragma unroll
         for (int k = 0; k < K3; ++k) add(s.c[k], 1.f);
 #if SK_BAR >= 1
@@ -223,6 +237,13 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&in, count * 4));
     CK(hipMalloc(&out, count * 4));
     CK(hipMalloc(&dummy, NT * 4));
+    float4* ringbuf = nullptr;
+    {
+        constexpr int K1h = ((TX + 2 * SK_M1) / 4 * (TY + 2 * SK_M1) + NT - 1) / NT;
+        const long nwg0 = (long)(n / TX) * (n / TY) * (n / 512);
+        CK(hipMalloc(&ringbuf, nwg0 * (2 * R + 1) * K1h * NT * sizeof(float4)));
+        CK(hipMemset(ringbuf, 0, nwg0 * (2 * R + 1) * K1h * NT * sizeof(float4)));
+    }
     fill_kernel<<<4096, 256>>>(in, count);
     CK(hipGetLastError());
     const int nwg = (n / TX) * (n / TY) * (n / zseg);
@@ -235,7 +256,7 @@ int main(int argc, char** argv) {
     const int reps = 7;
     for (int i = 0; i < reps + 1; ++i) {
         CK(hipEventRecord(a));
-        skeleton_kernel<<<nwg, NT, lds>>>(in, out, n, zseg, dummy);
+        skeleton_kernel<<<nwg, NT, lds>>>(in, out, n, zseg, dummy, ringbuf);
         CK(hipEventRecord(b));
         CK(hipEventSynchronize(b));
         CK(hipGetLastError());
@@ -247,8 +268,8 @@ int main(int argc, char** argv) {
         }
     }
     const double gb = (double)count * 8 / 1e9;
-    printf("skeleton TY=%d LDIST=%d NOSTORE=%d ST=%dx%d PAD=%d,%d STAUX=%d SK_BAR=%d SK_PF=%d TX=%d M1=%d noleave=%d noP3=%d noP5=%d lds=%d n=%d wg=%d: mean %.3f ms min %.3f ms (%.1f GB/s algorithmic)\n",
-           TY, SK_LDIST, SK_NOSTORE, STX, STY, SK_PADX, SK_PADY, SK_STAUX, SK_BAR, SK_PF, TX, SK_M1, SK_NOLEAVE, SK_NOP3, SK_NOP5, lds, n, nwg, sum / reps, best, gb / (sum / reps) * 1e3);
+    printf("skeleton RINGBUF=%d TY=%d LDIST=%d NOSTORE=%d ST=%dx%d PAD=%d,%d STAUX=%d SK_BAR=%d SK_PF=%d TX=%d M1=%d noleave=%d noP3=%d noP5=%d lds=%d n=%d wg=%d: mean %.3f ms min %.3f ms (%.1f GB/s algorithmic)\n",
+           SK_RINGBUF, TY, SK_LDIST, SK_NOSTORE, STX, STY, SK_PADX, SK_PADY, SK_STAUX, SK_BAR, SK_PF, TX, SK_M1, SK_NOLEAVE, SK_NOP3, SK_NOP5, lds, n, nwg, sum / reps, best, gb / (sum / reps) * 1e3);
     CK(hipFree(in));
     CK(hipFree(out));
     CK(hipFree(dummy));
