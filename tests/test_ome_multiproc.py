@@ -84,3 +84,11 @@ def test_copy_tree_equals_copytree(tmp_path, nthreads):
     np.testing.assert_array_equal(S.read_array(tmp_path / "a"), S.read_array(src))
     with pytest.raises(FileExistsError):
         ZO.copy_tree(str(src), str(tmp_path / "a"), nthreads)
+
+
+def test_row_spans_cut_at_the_chunk_grid():
+    from zarrs_tools_amd.zarrs_filter import _row_spans
+    assert _row_spans(0, 16, 8) == [(0, 8), (8, 16)]
+    assert _row_spans(5, 20, 8) == [(5, 8), (8, 16), (16, 24), (24, 25)]
+    assert _row_spans(31, 6, 8) == [(31, 32), (32, 37)]
+    assert _row_spans(3, 0, 8) == []

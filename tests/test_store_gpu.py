@@ -115,3 +115,44 @@ def test_downsample_store_mixed_stride_float_out(tmp_path):
     S.downsample(tmp_path / "in", tmp_path / "out", (3, 1, 2), data_type="float64")
     ref = O.downsample(v, "float32", (3, 1, 2), "float64")
     np.testing.assert_array_equal(S.read_array(tmp_path / "out"), ref)
+
+
+@pytest.mark.parametrize("dtype", ["uint16", "float32", "bfloat16"])
+def test_read_to_device_and_write_from_device_boxes(tmp_path, dtype):
+    """The pipelined store <-> HBM transfers of the device-resident paths (zarrs_filter
+    read_to_device / write_from_device: chunk rows decoded / encoded on a host thread while the
+    neighbouring row crosses PCIe through pinned buffers) give exactly the store's values, for the
+    whole array and for boxes whose rows start and end inside chunks."""
+    import torch
+    from zarrs_tools_amd.zarrs_filter import read_to_device, write_from_device
+    rng = np.random.default_rng(5)
+    shape, chunk = (37, 20, 30), (8, 8, 16)
+    store_dt = "uint16" if dtype == "bfloat16" else dtype
+    v = (rng.random(shape) * 60000).astype(store_dt)
+    make_input(tmp_path / "in", v, chunk, dtype=dtype)
+    want = S.read_array(tmp_path / "in")
+    for start, box in [(None, None), ((5, 3, 0), (20, 10, 30)), ((31, 0, 7), (6, 20, 9)),
+                       ((0, 0, 0), (1, 1, 1))]:
+        x = read_to_device(tmp_path / "in", 0, 4, start=start, shape=box)
+        if dtype == "bfloat16":
+            assert x.dtype == torch.bfloat16
+            x = x.view(torch.uint16)
+        sl = tuple(slice(a, a + n) for a, n in zip(start or (0, 0, 0), box or shape))
+        np.testing.assert_array_equal(x.cpu().numpy(), np.asarray(want)[sl])
+    # write a box and the whole array back
+    S.create_array(tmp_path / "out", dtype, shape, chunk)
+    whole = read_to_device(tmp_path / "in", 0, 4)
+    write_from_device(tmp_path / "out", whole, 4)
+    np.testing.assert_array_equal(S.read_array(tmp_path / "out"), want)
+    # a chunk-aligned box (its end may be the array's end), as the octant workers write
+    box = read_to_device(tmp_path / "in", 0, 4, start=(8, 0, 16), shape=(16, 16, 14))
+    S.create_array(tmp_path / "out2", dtype, shape, chunk)
+    write_from_device(tmp_path / "out2", box, 4, start=(8, 0, 16))
+    got = S.read_array(tmp_path / "out2")
+    np.testing.assert_array_equal(got[8:24, 0:16, 16:30], np.asarray(want)[8:24, 0:16, 16:30])
+    assert not got[:8].any() and not got[24:].any()  # untouched chunks read as the fill value
+    # the store writes whole chunks only (store_array_subset of whole chunks): an unaligned box
+    # is refused, not written partially
+    from zarrs_tools_amd._abi import InvalidParameters
+    with pytest.raises(InvalidParameters):
+        write_from_device(tmp_path / "out2", box[:5], 4, start=(9, 0, 16))
