@@ -300,6 +300,8 @@ def test_zarrs_ome_gpus_split_equals_one_process(tmp_path, gpus, mode):
                gpus=gpus, gpu_devices=[0] * gpus, **kw)
     if mode != "gaussian":
         assert b["stats"][0]["processes"] == gpus and b["stats"][0]["assembled_chunks"] > 0
+        # the octant workers run without torch (ZT_NO_TORCH=1, hiprt.py)
+        assert not any(r.get("torch_loaded") for r in b["stats"][0]["per_rank"])
     assert a["levels"] == b["levels"] >= 5
     for lvl in range(a["levels"] + 1):
         pa, pb = tmp_path / "one" / str(lvl), tmp_path / "many" / str(lvl)

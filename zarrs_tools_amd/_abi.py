@@ -108,11 +108,14 @@ def lib() -> ctypes.CDLL:
             f"{LIB_PATH} is missing: build it with `make -C zarrs_tools_amd/csrc` "
             "(or __graft_entry__.build()). There is no CPU fallback.")
     # torch ships its own libamdhip64 (same soname). Load it first so the process has exactly
-    # one HIP runtime: our NEEDED libamdhip64.so.7 then binds to the already-loaded copy.
-    try:
-        import torch  # noqa: F401
-    except ImportError:
-        pass
+    # one HIP runtime: our NEEDED libamdhip64.so.7 then binds to the already-loaded copy. A
+    # process that never uses torch (ZT_NO_TORCH=1: zarrs_ome's octant workers, hiprt.py) skips
+    # it and binds the ROCm runtime of the library's RUNPATH.
+    if os.environ.get("ZT_NO_TORCH") != "1":
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
     L = ctypes.CDLL(LIB_PATH)
     i64p = ctypes.POINTER(ctypes.c_int64)
     vp = ctypes.c_void_p

@@ -213,6 +213,92 @@ def _box_chunks(bstart, bshape, chunk, shape):
     return lo, hi, i0, i1
 
 
+def _box_levels_no_torch(lvl0: str, info0, assign, factor, discrete: bool, device: int,
+                         nthreads: int):
+    """The device part of an octant worker without torch (ZT_NO_TORCH=1, hiprt.py): the box of
+    level 0 streamed into HBM chunk row by chunk row (a host thread decodes row k+1 into one of
+    three pinned buffers while row k is copied on a stream, as read_to_device does), levels 1..L
+    by zt_pyramid_downsample (per-level zt_downsample_apply_ndarray past the fused levels, as
+    F.pyramid's callers do), and every level copied back to pinned host memory.
+    Returns (levels as numpy arrays, read seconds, kernel seconds, buffers to keep alive, phase
+    seconds)."""
+    import ctypes
+    from concurrent.futures import ThreadPoolExecutor
+    from . import filter as F
+    from . import hiprt as H
+    from .zarrs_filter import _row_spans
+    t0 = time.perf_counter()
+    H.set_device(device)
+    dt = info0.data_type
+    npdt = S.NUMPY[dt]
+    esz = np.dtype(npdt).itemsize
+    start, shape = [int(v) for v in assign.start], [int(v) for v in assign.shape]
+    nd = len(shape)
+    plane = int(np.prod(shape[1:])) if nd > 1 else 1
+    dev0 = H.DeviceBuffer(int(np.prod(shape)) * esz)
+    spans = _row_spans(start[0], shape[0], int(info0.chunk_shape[0]))
+    rows = max(b - a for a, b in spans)
+    nbuf = min(3, len(spans))
+    bufs = [H.PinnedBuffer(rows * plane * esz) for _ in range(nbuf)]
+    evs = [None] * nbuf
+    stream = H.Stream()
+    phases = {"setup_s": time.perf_counter() - t0}
+
+    def decode(k):
+        a, b = spans[k]
+        h = bufs[k % nbuf].array(npdt, [b - a] + shape[1:])
+        S.read_array(lvl0, [a] + start[1:], [b - a] + shape[1:], nthreads=nthreads, out=h)
+        return h
+
+    with ThreadPoolExecutor(1) as ex:
+        fut = ex.submit(decode, 0)
+        for k, (a, b) in enumerate(spans):
+            h = fut.result()
+            if k + 1 < len(spans):
+                if evs[(k + 1) % nbuf] is not None:
+                    evs[(k + 1) % nbuf].synchronize()  # its last H2D has finished
+                fut = ex.submit(decode, k + 1)
+            H.copy_async(dev0.at((a - start[0]) * plane * esz), ctypes.c_void_p(h.ctypes.data),
+                         (b - a) * plane * esz, H.H2D, stream)
+            ev = H.Event()
+            ev.record(stream)
+            evs[k % nbuf] = ev
+    stream.synchronize()
+    read_s = time.perf_counter() - t0
+    t1 = time.perf_counter()
+    L = assign.local_levels
+    ctx = F.Context(device)
+    shapes = F.pyramid_level_shapes(shape, factor, L)
+    outs = [H.DeviceBuffer(int(np.prod(sh)) * esz) for sh in shapes]
+    ptrs = (ctypes.c_void_p * max(len(outs), 1))(*[o.ptr.value for o in outs])
+    written = ctypes.c_int()
+    code = _abi.DTYPES[dt]
+    _abi.check(_abi.lib().zt_pyramid_downsample(
+        ctx.handle, code, dev0.ptr, _abi.i64_array(shape), nd, _abi.i64_array(factor), int(L),
+        int(discrete), ptrs, ctypes.byref(written)))
+    levels = [(outs[i], tuple(shapes[i])) for i in range(written.value)]
+    while len(levels) < L:  # the box's own stop rule ended early: one level at a time
+        src, sshape = levels[-1] if levels else (dev0, tuple(shape))
+        oshape = tuple(assign.level_boxes[len(levels)][1])
+        o = H.DeviceBuffer(int(np.prod(oshape)) * esz)
+        _abi.check(_abi.lib().zt_downsample_apply_ndarray(
+            ctx.handle, code, src.ptr, _abi.i64_array(sshape), nd, _abi.i64_array(factor),
+            int(discrete), code, o.ptr))
+        levels.append((o, oshape))
+    ctx.synchronize()
+    kernel_s = time.perf_counter() - t1
+    t2 = time.perf_counter()
+    keep, host = [], []
+    for buf, sh in levels:
+        pb = H.PinnedBuffer(int(np.prod(sh)) * esz)
+        H.copy_async(pb.ptr, buf.ptr, int(np.prod(sh)) * esz, H.D2H, stream)
+        keep.append(pb)
+        host.append(pb.array(npdt, sh))
+    stream.synchronize()
+    phases["d2h_s"] = time.perf_counter() - t2
+    return host, read_s, kernel_s, keep, phases
+
+
 def _octant_worker(out_root: str, assign, factor, discrete: bool, device: int, nthreads: int,
                    scratch: str, env=None, compute=None, src0=None) -> dict:
     """One process of `zarrs_ome --gpus N` (SURVEY.md §8(e) octant ownership): read this rank's
@@ -230,7 +316,16 @@ def _octant_worker(out_root: str, assign, factor, discrete: bool, device: int, n
     # level 0: the output's copy, or the input itself while the parent is still copying it
     lvl0 = src0 or os.path.join(out_root, "0")
     info0 = S.open_array(lvl0)
-    if compute is None:
+    keep = None
+    if compute is None and os.environ.get("ZT_NO_TORCH") == "1":
+        # a worker of octant_pool: no torch in this process (hiprt.py)
+        host, st["read_s"], st["kernel_s"], keep, ph = _box_levels_no_torch(
+            lvl0, info0, assign, list(factor), discrete, device, nthreads)
+        st.update(ph)
+        host_iter = iter(host)
+        cur = None
+        level, to_host = (lambda x: next(host_iter)), (lambda x: x)
+    elif compute is None:
         import torch
         from . import filter as F
         # the box streamed into HBM chunk row by chunk row (decode || H2D)
@@ -297,6 +392,8 @@ def _octant_worker(out_root: str, assign, factor, discrete: bool, device: int, n
             st["pieces"].append((k, tuple(cidx), tuple(p0), f))
         st["write_s"] += time.perf_counter() - t2
     st["wall_s"] = time.perf_counter() - t0
+    st["torch_loaded"] = "torch" in sys.modules
+    del keep  # the pinned level buffers, after their last use
     return st
 
 
@@ -336,13 +433,16 @@ def copy_tree(src: str, dst: str, nthreads: int = 0) -> None:
 
 
 def _octant_warmup(device: int) -> float:
-    """Run first on each pre-spawned octant worker (octant_pool): import torch and this package
-    and create the device's context while the parent still prepares the levels. The spawned
-    interpreter's start-up is most of a small rank's time."""
-    import torch
-    from . import filter as _F  # noqa: F401  (loads the HIP library)
-    if torch.cuda.is_available() and device < torch.cuda.device_count():
-        torch.empty(1, device=f"cuda:{device}")
+    """Run first on each pre-spawned octant worker (octant_pool): load the HIP library and create
+    the device's context while the parent still prepares the levels. The workers run without
+    torch (ZT_NO_TORCH=1, hiprt.py), whose import and runtime set-up were most of a small rank's
+    time."""
+    import ctypes
+    n = ctypes.c_int(0)
+    _abi.lib().zt_device_count(ctypes.byref(n))
+    if 0 <= device < n.value:
+        from . import hiprt
+        hiprt.set_device(device)
     return time.time()
 
 
@@ -352,8 +452,20 @@ def octant_pool(gpus: int, devices):
     import multiprocessing as mp
     from concurrent.futures import ProcessPoolExecutor
     ex = ProcessPoolExecutor(gpus, mp_context=mp.get_context("spawn"))
-    for d in list(devices)[:gpus]:
-        ex.submit(_octant_warmup, d)
+    # the workers never import torch (ZT_NO_TORCH=1 in the environment they are spawned with:
+    # processes start at submit, one per warm-up task; with no warm-up they start at the first
+    # task, inside the same setting)
+    old = os.environ.get("ZT_NO_TORCH")
+    if os.environ.get("ZT_OCTANT_TORCH") != "1":  # (=1: torch workers, for A/B runs)
+        os.environ["ZT_NO_TORCH"] = "1"
+    try:
+        for d in list(devices)[:gpus]:
+            ex.submit(_octant_warmup, d)
+    finally:
+        if old is None:
+            os.environ.pop("ZT_NO_TORCH", None)
+        else:
+            os.environ["ZT_NO_TORCH"] = old
     return ex
 
 
@@ -374,7 +486,7 @@ def run_octants(out_root: str, shape0, factor, levels, discrete: bool, gpus: int
     envs = [{"ZT_STORE_HOST_MEMORY": str(host_share)} for _ in range(gpus)]
     scratch = tempfile.mkdtemp(prefix=".zt_octants_", dir=out_root)
     t0 = time.perf_counter()
-    ex = pool if pool is not None else octant_pool(gpus, [])
+    ex = pool if pool is not None else octant_pool(gpus, devices)
     try:
         try:
             futs = [ex.submit(_octant_worker, out_root, assigns[g], list(factor), discrete,
