@@ -35,6 +35,7 @@ def hip() -> ctypes.CDLL:
             "hipHostMalloc": ([ctypes.POINTER(vp), sz, ctypes.c_uint], c_int),
             "hipHostFree": ([vp], c_int),
             "hipMemcpyAsync": ([vp, vp, sz, c_int, vp], c_int),
+            "hipMemcpy2DAsync": ([vp, sz, vp, sz, sz, sz, c_int, vp], c_int),
             "hipStreamCreate": ([ctypes.POINTER(vp)], c_int),
             "hipStreamDestroy": ([vp], c_int),
             "hipStreamSynchronize": ([vp], c_int),
@@ -156,3 +157,10 @@ class Event:
 
 def copy_async(dst, src, nbytes: int, kind: int, stream: Stream) -> None:
     check(hip().hipMemcpyAsync(dst, src, int(nbytes), int(kind), stream.handle), "hipMemcpyAsync")
+
+
+def copy2d_async(dst, dpitch: int, src, spitch: int, width: int, height: int, kind: int,
+                 stream: Stream) -> None:
+    """`height` rows of `width` bytes, row pitches `dpitch` / `spitch` (hipMemcpy2DAsync)."""
+    check(hip().hipMemcpy2DAsync(dst, int(dpitch), src, int(spitch), int(width), int(height),
+                                 int(kind), stream.handle), "hipMemcpy2DAsync")

@@ -236,30 +236,52 @@ def _box_levels_no_torch(lvl0: str, info0, assign, factor, discrete: bool, devic
     nd = len(shape)
     plane = int(np.prod(shape[1:])) if nd > 1 else 1
     dev0 = H.DeviceBuffer(int(np.prod(shape)) * esz)
+    # pieces: chunk rows of axis 0, cut along axis 1 at the chunk grid into pieces of about
+    # ZT_OCTANT_PIECE_KB (0: whole rows), so that each chunk is still decoded once but the
+    # pinned buffers hold a piece, not a whole row (3 x 2 GB per rank at 2048^3 u16)
     spans = _row_spans(start[0], shape[0], int(info0.chunk_shape[0]))
-    rows = max(b - a for a, b in spans)
-    nbuf = min(3, len(spans))
-    bufs = [H.PinnedBuffer(rows * plane * esz) for _ in range(nbuf)]
+    target = int(os.environ.get("ZT_OCTANT_PIECE_KB", "0")) << 10
+    plane2 = int(np.prod(shape[2:])) if nd > 2 else 1
+    pieces = []
+    for a, b in spans:
+        if nd >= 2 and target > 0:
+            cy = int(info0.chunk_shape[1])
+            m = max(1, target // max(1, (b - a) * cy * plane2 * esz))
+            pieces += [(a, b, ya, yb) for ya, yb in _row_spans(start[1], shape[1], cy * m)]
+        else:
+            pieces.append((a, b, start[1] if nd >= 2 else 0, start[1] + shape[1] if nd >= 2 else 1))
+    piece_elems = [(b - a) * (yb - ya) * plane2 if nd >= 2 else (b - a)
+                   for a, b, ya, yb in pieces]
+    nbuf = min(3, len(pieces))
+    bufs = [H.PinnedBuffer(max(piece_elems) * esz) for _ in range(nbuf)]
     evs = [None] * nbuf
     stream = H.Stream()
-    phases = {"setup_s": time.perf_counter() - t0}
+    phases = {"setup_s": time.perf_counter() - t0, "pieces": len(pieces)}
 
     def decode(k):
-        a, b = spans[k]
-        h = bufs[k % nbuf].array(npdt, [b - a] + shape[1:])
-        S.read_array(lvl0, [a] + start[1:], [b - a] + shape[1:], nthreads=nthreads, out=h)
+        a, b, ya, yb = pieces[k]
+        pshape = [b - a, yb - ya] + shape[2:] if nd >= 2 else [b - a]
+        pstart = [a, ya] + start[2:] if nd >= 2 else [a]
+        h = bufs[k % nbuf].array(npdt, pshape)
+        S.read_array(lvl0, pstart, pshape, nthreads=nthreads, out=h)
         return h
 
     with ThreadPoolExecutor(1) as ex:
         fut = ex.submit(decode, 0)
-        for k, (a, b) in enumerate(spans):
+        for k, (a, b, ya, yb) in enumerate(pieces):
             h = fut.result()
-            if k + 1 < len(spans):
+            if k + 1 < len(pieces):
                 if evs[(k + 1) % nbuf] is not None:
                     evs[(k + 1) % nbuf].synchronize()  # its last H2D has finished
                 fut = ex.submit(decode, k + 1)
-            H.copy_async(dev0.at((a - start[0]) * plane * esz), ctypes.c_void_p(h.ctypes.data),
-                         (b - a) * plane * esz, H.H2D, stream)
+            src = ctypes.c_void_p(h.ctypes.data)
+            if nd >= 2 and yb - ya < shape[1]:  # the piece's rows land with the box's pitch
+                width = (yb - ya) * plane2 * esz
+                H.copy2d_async(dev0.at(((a - start[0]) * shape[1] + (ya - start[1])) * plane2 * esz),
+                               shape[1] * plane2 * esz, src, width, width, b - a, H.H2D, stream)
+            else:  # whole rows: one contiguous copy
+                H.copy_async(dev0.at((a - start[0]) * plane * esz), src, (b - a) * plane * esz,
+                             H.H2D, stream)
             ev = H.Event()
             ev.record(stream)
             evs[k % nbuf] = ev
