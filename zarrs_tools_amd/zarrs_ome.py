@@ -256,7 +256,7 @@ def _box_levels_no_torch(lvl0: str, info0, assign, factor, discrete: bool, devic
     bufs = [H.PinnedBuffer(max(piece_elems) * esz) for _ in range(nbuf)]
     evs = [None] * nbuf
     stream = H.Stream()
-    phases = {"setup_s": time.perf_counter() - t0, "pieces": len(pieces)}
+    phases = {"setup_s": time.perf_counter() - t0, "read_pieces": len(pieces)}
 
     def decode(k):
         a, b, ya, yb = pieces[k]
