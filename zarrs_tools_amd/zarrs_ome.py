@@ -237,10 +237,11 @@ def _box_levels_no_torch(lvl0: str, info0, assign, factor, discrete: bool, devic
     plane = int(np.prod(shape[1:])) if nd > 1 else 1
     dev0 = H.DeviceBuffer(int(np.prod(shape)) * esz)
     # pieces: chunk rows of axis 0, cut along axis 1 at the chunk grid into pieces of about
-    # ZT_OCTANT_PIECE_KB (0: whole rows), so that each chunk is still decoded once but the
-    # pinned buffers hold a piece, not a whole row (3 x 2 GB per rank at 2048^3 u16)
+    # ZT_OCTANT_PIECE_KB (default 512 MiB; 0: whole rows). Each chunk is still decoded once, but
+    # the pinned buffers hold a piece, not a whole row: pinning 3 x 2 GB per rank made the box
+    # read 2x slower at 2048^3 u16 (profiles/r04_octant_workers*.json)
     spans = _row_spans(start[0], shape[0], int(info0.chunk_shape[0]))
-    target = int(os.environ.get("ZT_OCTANT_PIECE_KB", "0")) << 10
+    target = int(os.environ.get("ZT_OCTANT_PIECE_KB", "524288")) << 10
     plane2 = int(np.prod(shape[2:])) if nd > 2 else 1
     pieces = []
     for a, b in spans:
