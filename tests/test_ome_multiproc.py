@@ -92,3 +92,20 @@ def test_row_spans_cut_at_the_chunk_grid():
     assert _row_spans(5, 20, 8) == [(5, 8), (8, 16), (16, 24), (24, 25)]
     assert _row_spans(31, 6, 8) == [(31, 32), (32, 37)]
     assert _row_spans(3, 0, 8) == []
+
+
+def test_read_pieces_are_chunk_aligned_and_cover_the_box(monkeypatch):
+    from zarrs_tools_amd.zarrs_filter import _read_pieces
+    start, shape, chunk = (5, 3, 0), (40, 37, 30), (8, 8, 16)
+    whole = _read_pieces(start, shape, chunk, 2)  # default 512 MiB: whole chunk rows
+    assert [(a, b) for a, b, _, _ in whole] == [(5, 8), (8, 16), (16, 24), (24, 32), (32, 40),
+                                                (40, 45)]
+    assert all((ya, yb) == (3, 40) for _, _, ya, yb in whole)
+    monkeypatch.setenv("ZT_READ_PIECE_KB", "1")
+    small = _read_pieces(start, shape, chunk, 2)
+    cover = np.zeros(shape[:2], dtype=int)
+    for a, b, ya, yb in small:
+        assert (ya % 8 == 0 or ya == 3) and (yb % 8 == 0 or yb == 40)  # chunk grid / box ends
+        cover[a - 5:b - 5, ya - 3:yb - 3] += 1
+    assert (cover == 1).all()
+    assert _read_pieces((0,), (20,), (8,), 4) == [(0, 8, 0, 1), (8, 16, 0, 1), (16, 20, 0, 1)]

@@ -117,14 +117,17 @@ def test_downsample_store_mixed_stride_float_out(tmp_path):
     np.testing.assert_array_equal(S.read_array(tmp_path / "out"), ref)
 
 
-@pytest.mark.parametrize("dtype", ["uint16", "float32", "bfloat16"])
-def test_read_to_device_and_write_from_device_boxes(tmp_path, dtype):
+@pytest.mark.parametrize("dtype,piece_kb", [("uint16", None), ("float32", None),
+                                            ("bfloat16", None), ("uint16", "1")])
+def test_read_to_device_and_write_from_device_boxes(tmp_path, monkeypatch, dtype, piece_kb):
     """The pipelined store <-> HBM transfers of the device-resident paths (zarrs_filter
     read_to_device / write_from_device: chunk rows decoded / encoded on a host thread while the
     neighbouring row crosses PCIe through pinned buffers) give exactly the store's values, for the
     whole array and for boxes whose rows start and end inside chunks."""
     import torch
     from zarrs_tools_amd.zarrs_filter import read_to_device, write_from_device
+    if piece_kb:  # pieces of one chunk along axis 1: strided copies into the device box
+        monkeypatch.setenv("ZT_READ_PIECE_KB", piece_kb)
     rng = np.random.default_rng(5)
     shape, chunk = (37, 20, 30), (8, 8, 16)
     store_dt = "uint16" if dtype == "bfloat16" else dtype

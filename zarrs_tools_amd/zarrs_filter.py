@@ -261,6 +261,29 @@ def _row_spans(start0: int, n0: int, chunk0: int) -> list:
     return spans
 
 
+def _read_pieces(start, shape, chunk_shape, esz: int) -> list:
+    """The pieces a box read is pipelined in: chunk rows of axis 0, cut along axis 1 at the chunk
+    grid into pieces of about ZT_READ_PIECE_KB (default 512 MiB; 0: whole rows). Each chunk is
+    still decoded once, but a pinned buffer holds a piece instead of a whole chunk row: pinning
+    three 2 GB rows per process made 2048^3 u16 box reads 2x slower
+    (profiles/r04_octant_workers*.json). [(a, b, ya, yb)]; ya, yb = 0, 1 for 1-D arrays."""
+    nd = len(shape)
+    spans = _row_spans(start[0], shape[0], int(chunk_shape[0])) if shape[0] > 0 else []
+    if nd < 2:
+        return [(a, b, 0, 1) for a, b in spans]
+    target = int(os.environ.get("ZT_READ_PIECE_KB", "524288")) << 10
+    plane2 = int(np.prod(shape[2:])) if nd > 2 else 1
+    cy = int(chunk_shape[1])
+    out = []
+    for a, b in spans:
+        if target > 0:
+            m = max(1, target // max(1, (b - a) * cy * plane2 * esz))
+            out += [(a, b, ya, yb) for ya, yb in _row_spans(start[1], shape[1], cy * m)]
+        else:
+            out.append((a, b, start[1], start[1] + shape[1]))
+    return out
+
+
 def read_to_device(path, device: int, nthreads: int = 0, start=None, shape=None):
     """The box [start, start + shape) of a store array (the whole array by default) decoded into
     HBM, overlapped chunk row by chunk row: a host thread decodes row k+1
@@ -278,33 +301,42 @@ def read_to_device(path, device: int, nthreads: int = 0, start=None, shape=None)
     tdt = F.torch_dtype(store_dt)
     dev = torch.device("cuda", device)
     x = torch.empty(tuple(shape), dtype=tdt, device=dev)
-    spans = _row_spans(start[0], shape[0], int(info.chunk_shape[0])) if shape[0] > 0 else []
-    if spans and all(v > 0 for v in shape):
-        plane = int(np.prod(shape[1:])) if nd > 1 else 1
-        rows = max(b - a for a, b in spans)
-        nbuf = min(3, len(spans))
-        bufs = [torch.empty((rows * plane,), dtype=tdt, pin_memory=True) for _ in range(nbuf)]
+    if all(v > 0 for v in shape):
+        pieces = _read_pieces(start, shape, info.chunk_shape, x.element_size())
+
+        def pshape(p):
+            a, b, ya, yb = p
+            return [b - a, yb - ya] + shape[2:] if nd >= 2 else [b - a]
+
+        n_max = max(int(np.prod(pshape(p))) for p in pieces)
+        nbuf = min(3, len(pieces))
+        bufs = [torch.empty((n_max,), dtype=tdt, pin_memory=True) for _ in range(nbuf)]
         evs = [None] * nbuf
         stream = torch.cuda.Stream(device=dev)
 
         def decode(k):
-            a, b = spans[k]
-            h = bufs[k % nbuf][:(b - a) * plane].view([b - a] + shape[1:])
-            S.read_array(path, [a] + start[1:], [b - a] + shape[1:], nthreads=nthreads,
+            a, b, ya, yb = pieces[k]
+            ps = pshape(pieces[k])
+            h = bufs[k % nbuf][:int(np.prod(ps))].view(ps)
+            S.read_array(path, [a, ya] + start[2:] if nd >= 2 else [a], ps, nthreads=nthreads,
                          out=h.numpy())
             return h
 
         with ThreadPoolExecutor(1) as ex:
             fut = ex.submit(decode, 0)
-            for k, (a, b) in enumerate(spans):
+            for k, (a, b, ya, yb) in enumerate(pieces):
                 h = fut.result()
-                if k + 1 < len(spans):
+                if k + 1 < len(pieces):
                     ev = evs[(k + 1) % nbuf]
                     if ev is not None:
                         ev.synchronize()  # the H2D that last read this buffer has finished
                     fut = ex.submit(decode, k + 1)
                 with torch.cuda.stream(stream):
-                    x[a - start[0]:b - start[0]].copy_(h, non_blocking=True)
+                    if nd >= 2:
+                        x[a - start[0]:b - start[0], ya - start[1]:yb - start[1]].copy_(
+                            h, non_blocking=True)
+                    else:
+                        x[a - start[0]:b - start[0]].copy_(h, non_blocking=True)
                     ev = torch.cuda.Event()
                     ev.record(stream)
                 evs[k % nbuf] = ev

@@ -226,7 +226,7 @@ def _box_levels_no_torch(lvl0: str, info0, assign, factor, discrete: bool, devic
     from concurrent.futures import ThreadPoolExecutor
     from . import filter as F
     from . import hiprt as H
-    from .zarrs_filter import _row_spans
+    from .zarrs_filter import _read_pieces
     t0 = time.perf_counter()
     H.set_device(device)
     dt = info0.data_type
@@ -236,21 +236,9 @@ def _box_levels_no_torch(lvl0: str, info0, assign, factor, discrete: bool, devic
     nd = len(shape)
     plane = int(np.prod(shape[1:])) if nd > 1 else 1
     dev0 = H.DeviceBuffer(int(np.prod(shape)) * esz)
-    # pieces: chunk rows of axis 0, cut along axis 1 at the chunk grid into pieces of about
-    # ZT_OCTANT_PIECE_KB (default 512 MiB; 0: whole rows). Each chunk is still decoded once, but
-    # the pinned buffers hold a piece, not a whole row: pinning 3 x 2 GB per rank made the box
-    # read 2x slower at 2048^3 u16 (profiles/r04_octant_workers*.json)
-    spans = _row_spans(start[0], shape[0], int(info0.chunk_shape[0]))
-    target = int(os.environ.get("ZT_OCTANT_PIECE_KB", "524288")) << 10
+    # pieces of about 512 MiB, each chunk decoded once (zarrs_filter._read_pieces)
+    pieces = _read_pieces(start, shape, info0.chunk_shape, esz)
     plane2 = int(np.prod(shape[2:])) if nd > 2 else 1
-    pieces = []
-    for a, b in spans:
-        if nd >= 2 and target > 0:
-            cy = int(info0.chunk_shape[1])
-            m = max(1, target // max(1, (b - a) * cy * plane2 * esz))
-            pieces += [(a, b, ya, yb) for ya, yb in _row_spans(start[1], shape[1], cy * m)]
-        else:
-            pieces.append((a, b, start[1] if nd >= 2 else 0, start[1] + shape[1] if nd >= 2 else 1))
     piece_elems = [(b - a) * (yb - ya) * plane2 if nd >= 2 else (b - a)
                    for a, b, ya, yb in pieces]
     nbuf = min(3, len(pieces))
