@@ -43,15 +43,6 @@
 #ifndef GF_STY
 #define GF_STY 16  // XCD super-tile: tiles along y
 #endif
-#ifndef GF_PERS
-#define GF_PERS 1  // persistent XCD-group schedule for mode-1 grids (see GFParams)
-#endif
-#ifndef GF_LOCK
-#define GF_LOCK 0  // lockstep lead bound in steps (0: off)
-#endif
-#ifndef GF_PERS_STX
-#define GF_PERS_STX 4  // super-tile width in tiles (height = workgroups per XCD / width)
-#endif
 #ifndef GF_WAVE_SKIP
 #define GF_WAVE_SKIP 1  // P4: idle waves branch around the phase
 #endif
@@ -576,7 +567,7 @@ struct GFConfig {
 // instructions, so the compiler's vmcnt accounting stays exact (a branch there made it drain
 // every load).
 template <int R, int TY, int NT, typename TIn, typename TOut, int MODE>
-__global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p_arg) {
+__global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     using C = GFConfig<R, TY, NT, S1<TIn>::HXB>;
     using SA = typename S1<TIn>::acc;  // stage-1 window sums (exact)
     using SI = typename S1<TIn>::in;   // loaded stage-1 values
@@ -593,93 +584,46 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p_arg) {
     // (Markstein's correction needs RN(1/c) exactly). Published by the prologue's barrier.
     for (int c = threadIdx.x; c <= C::W3; c += NT) rcp_tab[c] = c > 0 ? 1.0f / (float)c : 0.0f;
 
-
-    // Unit range of this workgroup: one unit (a tile over one z-segment) in the regular grid; a
-    // run of super-tile units in the persistent schedule (MODE 1 only, see GFParams), where every
-    // workgroup of XCD group g starts unit u when it has finished unit u - 1, so the group's
-    // tiles march the same z-range together and the union of their aprons stays in the XCD's L2.
-    const bool pers = p_arg.pers_stx > 0;
-    const int pg = blockIdx.x % 8, pj = blockIdx.x / 8;
-    int u = 0, ue = 1;
-    if (pers) {
-        u = (int)((int64_t)pg * p_arg.pers_units / 8);
-        ue = (int)((int64_t)(pg + 1) * p_arg.pers_units / 8);
-        if (pj >= p_arg.pers_stx * p_arg.pers_sty) ue = u;
-    }
-    // lockstep state (GF_LOCK): steps done by this workgroup in this launch, the group's slots
-    // as polled one step ago, and whether waiting is still on (a timed-out wait turns it off)
-    unsigned lk_steps = p_arg.pers_epoch << 24;
-    unsigned lk_poll = lk_steps;
-    bool lk_on = GF_LOCK > 0 && pers && p_arg.pers_sync != nullptr;
-    const int lk_slots = p_arg.pers_stx * p_arg.pers_sty;
-    const rsrc_t lk_rs = make_rsrc(p_arg.pers_sync + 64 * pg, lk_on ? 256u : 0u);
-    const int lane = (int)(threadIdx.x & 63);
-    const int lk_pub = threadIdx.x == 0 ? 4 * pj : kBadOff;
-    const int lk_get = lane < lk_slots ? 4 * lane : kBadOff;
-    for (; u < ue; ++u) {
-        // The parameters are re-read per unit through a pointer the optimiser cannot see
-        // through: otherwise it hoists every unit-invariant product of them out of the unit loop
-        // and the march runs out of SGPRs (hundreds of spills to VGPR lanes).
-        // (GFParams is the kernel's only argument: it sits at the start of the kernarg segment,
-        // and the reads stay scalar loads of that constant segment.)
-        typedef const __attribute__((address_space(4))) GFParams KParams;
-        KParams* pq = (KParams*)__builtin_amdgcn_kernarg_segment_ptr();
-        __asm__ volatile("" : "+s"(pq));
-        KParams& p = *pq;
-        int tile_x, tile_y, seg;
-        if (pers) {
-            const int s = u / p.nseg;
-            seg = u % p.nseg;
-            tile_x = (s % p.pers_nsx) * p.pers_stx + pj % p.pers_stx;
-            tile_y = (s / p.pers_nsx) * p.pers_sty + pj / p.pers_stx;
-            if (tile_x >= p.tiles_x || tile_y >= p.tiles_y) {
-                // (the group's other tiles march this unit: keep the step count aligned)
-                const int zb0 = p.oz0 + seg * p.zseg, ze0 = min(zb0 + p.zseg, p.oz0 + p.onz);
-                lk_steps += (ze0 - zb0 + 2 * R + 1 + C::W - 1) / C::W * C::W;
-                continue;
+    // XCD-aware block -> tile. Blocks b and b+8 share an XCD; give each XCD a contiguous run of
+    // logical ids and walk them in GF_STX x GF_STY-tile super-tiles, so the WGs resident on one
+    // XCD cover a compact region whose xy aprons and z reloads stay in that XCD's 4 MB L2.
+    const int nwg = gridDim.x;
+    const int b = blockIdx.x;
+    const int lid = (nwg % 8 == 0) ? (b % 8) * (nwg / 8) + b / 8 : b;
+    const int gtx = INTERIOR ? p.itx1 - p.itx0 : p.tiles_x;  // this launch's tile grid
+    const int gty = INTERIOR ? p.ity1 - p.ity0 : p.tiles_y;
+    const int ntiles = gtx * gty;
+    const int seg = lid / ntiles;
+    int t = lid % ntiles;
+    int tile_x, tile_y;
+    {
+        const int stx = GF_STX, sty = GF_STY;
+        const int full_y = gty / sty * sty;
+        const int per_srow = gtx * sty;
+        if (t < full_y * gtx) {
+            const int sr = t / per_srow, r = t % per_srow;
+            const int full_x = gtx / stx * stx;
+            if (r < full_x * sty) {
+                tile_x = (r / (stx * sty)) * stx + r % stx;
+                tile_y = sr * sty + (r / stx) % sty;
+            } else {
+                const int rr = r - full_x * sty, w = gtx - full_x;
+                tile_x = full_x + rr % w;
+                tile_y = sr * sty + rr / w;
             }
         } else {
-            // XCD-aware block -> tile. Blocks b and b+8 share an XCD; give each XCD a contiguous
-            // run of logical ids and walk them in GF_STX x GF_STY-tile super-tiles, so the WGs
-            // resident on one XCD cover a compact region whose xy aprons and z reloads stay in
-            // that XCD's 4 MB L2.
-            const int nwg = gridDim.x;
-            const int b = blockIdx.x;
-            const int lid = (nwg % 8 == 0) ? (b % 8) * (nwg / 8) + b / 8 : b;
-            const int gtx = INTERIOR ? p.itx1 - p.itx0 : p.tiles_x;  // this launch's tile grid
-            const int gty = INTERIOR ? p.ity1 - p.ity0 : p.tiles_y;
-            const int ntiles = gtx * gty;
-            seg = lid / ntiles;
-            int t = lid % ntiles;
-            const int stx = GF_STX, sty = GF_STY;
-            const int full_y = gty / sty * sty;
-            const int per_srow = gtx * sty;
-            if (t < full_y * gtx) {
-                const int sr = t / per_srow, r = t % per_srow;
-                const int full_x = gtx / stx * stx;
-                if (r < full_x * sty) {
-                    tile_x = (r / (stx * sty)) * stx + r % stx;
-                    tile_y = sr * sty + (r / stx) % sty;
-                } else {
-                    const int rr = r - full_x * sty, w = gtx - full_x;
-                    tile_x = full_x + rr % w;
-                    tile_y = sr * sty + rr / w;
-                }
-            } else {
-                t -= full_y * gtx;
-                tile_x = t % gtx;
-                tile_y = full_y + t / gtx;
-            }
-            if constexpr (INTERIOR) {
-                tile_x += p.itx0;
-                tile_y += p.ity0;
-            } else {
-                if (tile_x >= p.itx0 && tile_x < p.itx1 && tile_y >= p.ity0 && tile_y < p.ity1)
-                    continue;
-            }
+            t -= full_y * gtx;
+            tile_x = t % gtx;
+            tile_y = full_y + t / gtx;
         }
-        // One march: output tile (tile_x, tile_y) over z-segment seg.
-        auto march = [&](const int tile_x, const int tile_y, const int seg) {
+    }
+    if constexpr (INTERIOR) {
+        tile_x += p.itx0;
+        tile_y += p.ity0;
+    } else {
+        if (tile_x >= p.itx0 && tile_x < p.itx1 && tile_y >= p.ity0 && tile_y < p.ity1) return;
+    }
+
     const int x0 = p.ox0 + tile_x * TX;
     const int y0 = p.oy0 + tile_y * TY;
     const int ox_end = p.ox0 + p.onx, oy_end = p.oy0 + p.ony;
@@ -1123,25 +1067,6 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p_arg) {
             constexpr int k = decltype(kc)::value;
             const int i = i0 + k;
             const int tid = threadIdx.x;
-            if constexpr (GF_LOCK > 0) {
-                // publish this step, wait while this workgroup leads a member of its group by
-                // more than GF_LOCK steps (by the slots polled a step ago), then poll again
-                auto ahead = [&](unsigned v) {
-                    return __ballot(lane < lk_slots && (int)(lk_steps - v) > GF_LOCK) != 0;
-                };
-                ++lk_steps;
-                __builtin_amdgcn_raw_buffer_store_b32(lk_steps, lk_rs, opaque(lk_pub), 0, 0);
-                if (lk_on && ahead(lk_poll)) {
-                    int it = 0;
-                    for (; it < 64; ++it) {
-                        __builtin_amdgcn_s_sleep(2);
-                        if (!ahead(__builtin_amdgcn_raw_buffer_load_b32(lk_rs, lk_get, 0, 16)))
-                            break;
-                    }
-                    if (it == 64) lk_on = false;
-                }
-                lk_poll = __builtin_amdgcn_raw_buffer_load_b32(lk_rs, opaque(lk_get), 0, 16);
-            }
             const rsrc_t r_b = rs_in(ob, zb);
             ro5 = make_rsrc(out_base + os, (unsigned)(zs - zo_begin) < nzo ? oslice_bytes : 0u);
             // Fair progress across the waves of a SIMD: the hardware issues oldest-first, which
@@ -1172,12 +1097,6 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p_arg) {
             os += osstride;
         });
     }
-    };  // march
-        march(tile_x, tile_y, seg);
-    }
-    if constexpr (GF_LOCK > 0)  // done: never make the group wait for this workgroup again
-        __builtin_amdgcn_raw_buffer_store_b32((p_arg.pers_epoch << 24) | 0xFFFFFFu, lk_rs,
-                                              opaque(lk_pub), 0, 0);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1231,73 +1150,6 @@ inline hipError_t launch_fused_variant(const GFParams& p, long long nwg, hipStre
     return hipGetLastError();
 }
 
-// Compute units of the current device (cached per device).
-inline int device_cu_count() {
-    static std::atomic<int> cache[64];
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return 0;
-    std::atomic<int>& c = cache[dev & 63];
-    int n = c.load(std::memory_order_relaxed);
-    if (n == 0) {
-        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            return 0;
-        c.store(n, std::memory_order_relaxed);
-    }
-    return n;
-}
-
-
-// The persistent schedule for a mode-1 grid: one workgroup per CU, XCD group g marching the
-// super-tiles of its contiguous unit range. z-segments are chosen to balance the 8 groups: the
-// cost of a segmentation is (units per group) x (steps per march incl. the 2R + 1 warm-up and the
-// padding to a multiple of 2R + 1). Returns the grid size, or 0 when the volume is too small for
-// whole super-tiles to keep the groups busy (the regular grid is used then).
-template <int R, int TY>
-inline long long persistent_plan(GFParams& p) {
-    constexpr int W = 2 * R + 1;
-    const int ncu = device_cu_count();
-    if (!GF_PERS || ncu < 64 || ncu % 8 != 0) return 0;
-    const int P = ncu / 8, stx = GF_PERS_STX, sty = P / stx;
-    if (sty < 1) return 0;
-    const long long nsx = (p.tiles_x + stx - 1) / stx, nsy = (p.tiles_y + sty - 1) / sty;
-    // idle slots of partial super-tiles
-    if ((long long)p.tiles_x * p.tiles_y * 4 < nsx * stx * nsy * sty * 3) return 0;
-    long long best = -1, best_nseg = 1;
-    for (long long nseg = 1; nseg <= 64 && nseg <= p.onz; ++nseg) {
-        const long long zseg = (p.onz + nseg - 1) / nseg;
-        const long long ns = (p.onz + zseg - 1) / zseg;
-        const long long units = nsx * nsy * ns;
-        const long long per_group = (units + 7) / 8;
-        const long long steps = (zseg + 2 * R + 1 + W - 1) / W * W + 2 * R + 1;
-        const long long cost = per_group * steps;
-        if (best < 0 || cost < best) { best = cost; best_nseg = nseg; }
-    }
-    p.zseg = (int)((p.onz + best_nseg - 1) / best_nseg);
-    p.nseg = (p.onz + p.zseg - 1) / p.zseg;
-    const long long units = nsx * nsy * p.nseg;
-    if (units < 8) return 0;
-    if (GF_LOCK > 0) {
-        // per-device group slots (8 x 64 words), allocated once; an epoch per launch tells this
-        // launch's slot values from an earlier launch's
-        static unsigned* bufs[64] = {};
-        static std::atomic<unsigned> epoch{0};
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess) return 0;
-        unsigned*& b = bufs[dev & 63];
-        if (!b) {
-            if (hipMalloc(&b, 8 * 64 * sizeof(unsigned)) != hipSuccess) { b = nullptr; return 0; }
-            if (hipMemset(b, 0, 8 * 64 * sizeof(unsigned)) != hipSuccess) return 0;
-        }
-        p.pers_sync = b;
-        p.pers_epoch = (epoch.fetch_add(1) + 1) & 0xFF;
-    }
-    p.pers_stx = stx;
-    p.pers_sty = sty;
-    p.pers_nsx = (int)nsx;
-    p.pers_units = (int)units;
-    return 8LL * P;
-}
-
 template <int R, int TY, int NT, typename TIn, typename TOut>
 inline hipError_t launch_fused_cfg(const GFParams& p0, hipStream_t stream) {
     using C = GFConfig<R, TY, NT>;
@@ -1310,7 +1162,6 @@ inline hipError_t launch_fused_cfg(const GFParams& p0, hipStream_t stream) {
     p.tiles_x = (p.onx + C::TX - 1) / C::TX;
     p.tiles_y = (p.ony + TY - 1) / TY;
     p.nseg = (p.onz + p.zseg - 1) / p.zseg;
-    p.pers_stx = p.pers_sty = p.pers_nsx = p.pers_units = 0;
     // Interior tiles (mode 0): the whole E2 apron inside the domain, the tile inside the output
     // box. Quad-aligned geometry (every quad starts at a multiple of 4 elements: the E2 apron at
     // x0 - 2R, the output tile at x0; the domain / output box widths multiples of 4): no quad
@@ -1327,9 +1178,6 @@ inline hipError_t launch_fused_cfg(const GFParams& p0, hipStream_t stream) {
         // choosing the class per workgroup (both marches in one kernel: more SGPR spills); mode 0
         // alone over every tile (border output wrong, a bound only) 29.1 ms.
         p.itx0 = p.itx1 = p.ity0 = p.ity1 = 0;
-        GFParams q = p;
-        if (const long long nwg = persistent_plan<R, TY>(q))
-            return launch_fused_variant<R, TY, NT, TIn, TOut, 1>(q, nwg, stream);
         return launch_fused_variant<R, TY, NT, TIn, TOut, 1>(p, n_all * p.nseg, stream);
     }
     interior_tiles(p.ox0, p.ox0 + p.onx, p.nx, C::TX, R, 0, p.tiles_x, p.itx0, p.itx1);

@@ -32,18 +32,6 @@ struct GFParams {
     int itx0, itx1, ity0, ity1;  // interior tile range (fused kernel, host-computed)
     float eps;
     float rcp_w3;  // RN(1 / (2r+1)^3): the interior window count's reciprocal (host-computed)
-    // Persistent schedule (pers_stx > 0; gf_fused.hpp): 8 * pers_wg workgroups, one per CU. Blocks
-    // b and b + 8 share an XCD, so XCD group g = b % 8 owns a contiguous run of units
-    // (super-tile-major, z-segment-minor); a unit is one pers_stx x pers_sty super-tile of tiles
-    // over one z-segment, and slot j = b / 8 of the group marches tile j of it. The group's
-    // workgroups start every unit together, so their xy aprons and z re-reads share the L2.
-    int pers_stx, pers_sty, pers_nsx, pers_units;
-    // Loose lockstep of a group (GF_LOCK): each workgroup publishes its step count in
-    // pers_sync[64 g + j] (epoch << 24 | steps) and waits while it leads a group member by more
-    // than GF_LOCK steps (bounded: after a timed-out wait it stops waiting). A speed hint only;
-    // no result depends on it. Null: no lockstep.
-    unsigned* pers_sync;
-    unsigned pers_epoch;
 };
 
 // N-d geometry for the separable path and downsample (C-order logical shapes).
