@@ -58,6 +58,11 @@ def parse():
                          "chunk rows (+ 2r halo) of the volume on this GPU (no process group)")
     ap.add_argument("--radius", type=int, default=RADIUS,
                     help="guided-filter radius (default 4 = the metric; 2 = config G2 at --size 1024)")
+    ap.add_argument("--no-extra", action="store_true",
+                    help="skip the other BASELINE configs timed after the headline (G2, the "
+                         "config-T share, the config-P octant pyramid, the Gaussian)")
+    ap.add_argument("--extra", default="g2,t_share,pyramid_octant,gaussian",
+                    help="comma list of the extra legs to run")
     return ap.parse_args()
 
 
@@ -114,7 +119,24 @@ def cpu_baseline(gshape, radius: int, nchunks: int = 0):
               for i in range(nchunks)]  # a diagonal walk through the grid (interior + edges)
     secs, vox = O.time_guided_filter_chunks(gshape, (CHUNK,) * 3, coords, EPS, radius, threads)
     gibs = vox * 4 / 2 ** 30 / secs
+    # The reference's rayon pool would take every CPU of the affinity (guided_filter.rs:261-316).
+    # A GPU box grants a share of its CPUs per GPU (OMP_NUM_THREADS), and worker pools stay within
+    # it, so the full-affinity figure is extrapolated: one thread on 2 chunks gives the per-core
+    # rate, the share run its parallel efficiency, and the estimate assumes that efficiency holds
+    # up to every CPU of the affinity (memory-bounded like calculate_chunk_limit, not checked).
+    full = None
+    aff = _affinity_count() or ncpu
+    if aff > threads:
+        s1, v1 = O.time_guided_filter_chunks(gshape, (CHUNK,) * 3, coords[:2], EPS, radius, 1)
+        g1 = v1 * 4 / 2 ** 30 / s1
+        eff = min(1.0, gibs / (threads * g1))
+        full = {"value": round(g1 * aff * eff, 4), "unit": "GiB/s", "cores": aff,
+                "kind": "extrapolated", "per_core_gibs": round(g1, 5),
+                "share_parallel_efficiency": round(eff, 3),
+                "sample": f"1 thread on 2 chunks ({s1:.2f} s); estimate = per-core rate x "
+                          f"{aff} CPUs x the {threads}-thread run's efficiency"}
     return {"value": round(gibs, 5), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "full_affinity": full,
             "host_cpus": ncpu, "affinity_cpus": _affinity_count(),
             "sample": f"{nchunks} chunks of 256^3 (r={radius}, 2r halo) of the same "
                       f"{'x'.join(map(str, gshape))} synthetic volume, {secs:.2f} s wall on "
@@ -169,6 +191,21 @@ def lib_hash() -> str:
     return h.hexdigest()
 
 
+def load_leg_traffic(leg: str):
+    """Per-launch-set HBM traffic of an extra leg (profiles/pmc_traffic.json entries with
+    "leg": name), only when measured on this exact library build; else None."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        for e in d.get("entries", []):
+            if e.get("leg") == leg and e.get("lib_sha256") == lib_hash():
+                return e.get("hbm_bytes_per_call")
+    except (OSError, ValueError, AttributeError):
+        pass
+    return None
+
+
 def load_traffic(gshape, radius: int, world: int, share=None):
     """Per-launch HBM traffic from the committed rocprofv3 PMC summary (profiles/pmc_traffic.json),
     only when it was measured on this exact library build and workload — the same global shape,
@@ -188,6 +225,200 @@ def load_traffic(gshape, radius: int, world: int, share=None):
     except (OSError, ValueError, AttributeError):
         pass
     return None
+
+
+# ---- the other BASELINE configs, timed after the headline on the same GPU -----------------------
+# Each leg: HIP-event time on the launch stream (inputs resident), its roofline against the
+# algorithmic bytes, the committed PMC traffic when keyed to this build, and a sampled parity
+# check against the oracle (after timing). Never part of the headline `value`.
+
+def _time_ms(fn, stream, warmup: int, reps: int) -> float:
+    import torch
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        fn()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def _roof(algo_bytes: int, ms: float, traffic):
+    gbs = algo_bytes / (ms / 1e3) / 1e9
+    r = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+         "frac": round(gbs / HBM_PEAK_GBS, 4), "algorithmic_bytes": int(algo_bytes),
+         "traffic": traffic}
+    if traffic:
+        r["traffic_gbs"] = round(traffic / (ms / 1e3) / 1e9, 1)
+    return r
+
+
+def _max_rel(got, ref) -> float:
+    import numpy as np
+    d = np.abs(got.astype(np.float64) - ref.astype(np.float64))
+    return float((d / np.maximum(1.0, np.abs(ref.astype(np.float64)))).max())
+
+
+def leg_g2(ctx, L, stream, warmup, reps):
+    """configs[1]: guided_filter r=2 on 1024^3 f32, 256^3 chunks, one fused launch."""
+    import torch
+    import zarrs_tools_amd as zt
+    from zarrs_tools_amd import _abi
+    from zarrs_tools_amd.filter import _ptr
+    size, radius = 1024, 2
+    gshape = (size,) * 3
+    a = zt.slab_assignment(0, 1, size, CHUNK, 2 * radius)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    slab = torch.empty((a.in_nz, size, size), dtype=torch.float32, device=dev)
+    out = torch.empty((a.out_nz, size, size), dtype=torch.float32, device=dev)
+    _abi.check(L.zt_synth_step_noise_f32(ctx.handle, _ptr(slab), _abi.i64_array(slab.shape), 3,
+                                         _abi.i64_array(gshape), a.in_z0, 0x5EED2025))
+    gs, cs = _abi.i64_array(gshape), _abi.i64_array((CHUNK,) * 3)
+
+    def step():
+        _abi.check(L.zt_guided_filter_apply_slab(ctx.handle, 11, _ptr(slab), 11, _ptr(out), gs,
+                                                 a.in_z0, a.in_nz, a.out_z0, a.out_nz, cs, EPS,
+                                                 radius))
+    ms = _time_ms(step, stream, warmup, reps)
+    vox = size ** 3
+    par = parity_sample(out, a, gshape, radius, 4)
+    return {"config": "BASELINE configs[1]: guided_filter r=2 on 1024^3 f32, 256^3 chunks, "
+                      "1 GPU device-resident", "ms": round(ms, 4),
+            "value": round(vox * 4 / 2 ** 30 / (ms / 1e3), 3), "unit": "GiB/s",
+            "roofline": _roof(vox * ALGO_BYTES_PER_VOXEL, ms, load_traffic(gshape, radius, 1)),
+            "parity": {k: par[k] for k in ("max_rel", "tol", "ok", "chunks", "bit_exact_frac")}}
+
+
+def leg_t_share(ctx, L, stream, warmup, reps):
+    """configs[4] per GPU: one rank's (t, z) block of the 8-GPU split of the (32, 1024^3) f32
+    series in (4, 256^3) chunks (shard.block_split: 2 t-groups x 4 z-groups; an interior rank:
+    16 output timepoints x 256 planes from 20 x 264 input planes), r=2, eps 2500, one
+    GuidedFilter::apply_ndarray call on its halo'd box (the 4-D three-kernel path)."""
+    import numpy as np
+    import torch
+    import zarrs_tools_amd as zt
+    from zarrs_tools_amd import shard
+    from zarrs_tools_amd.filter import ArraySubset
+    from oracle import oracle as O
+    gshape, chunk, world, radius = (32, 1024, 1024, 1024), (4, 256, 256, 256), 8, 2
+    groups = shard.block_split(world, gshape, chunk, 2 * radius)
+    rank = (groups[0] // 2) * groups[1] + groups[1] // 2
+    a = shard.block_assignment(rank, world, gshape, chunk, 2 * radius, groups)
+    x = zt.synth_box(a.in_start, a.in_shape, gshape, kind="float32", ctx=ctx)
+    rel0 = tuple(o - i for o, i in zip(a.out_start, a.in_start))
+    g = zt.GuidedFilter(EPS, radius)
+    sub = ArraySubset(rel0, a.out_shape)
+    res = {}
+
+    def step():
+        res["y"] = None  # the caching allocator hands the same block back
+        res["y"] = g.apply_ndarray(x, sub, ctx=ctx)
+    ms = _time_ms(step, stream, warmup, reps)
+    y = res.pop("y")
+    n = int(np.prod(a.out_shape))
+    # parity: sampled (4, 32, 32, 32) output boxes (corner and interior of the share) against the
+    # oracle's apply_ndarray on the box + its 2r halo from the global synthetic series (the
+    # chunked result equals the whole-array one, tests/test_oracle.py)
+    box = (4, 32, 32, 32)
+    starts = [tuple(a.out_start), tuple(o + s // 2 for o, s in zip(a.out_start, a.out_shape)),
+              tuple(o + s - b for o, s, b in zip(a.out_start, a.out_shape, box))]
+    coords = [tuple(st // b for st, b in zip(s0, box)) for s0 in starts]
+    worst = 0.0
+    for (o0, osh, ref) in O.guided_filter_synth_chunks(gshape, box, coords, EPS, radius,
+                                                       nthreads=len(coords)):
+        sl = tuple(slice(p - q, p - q + s) for p, q, s in zip(o0, a.out_start, osh))
+        worst = max(worst, _max_rel(y[sl].cpu().numpy(), ref))
+    del x, y
+    ctx.release_scratch()
+    torch.cuda.empty_cache()
+    return {"config": "BASELINE configs[4] per GPU: rank %d's (t, z) block of the 8-GPU split "
+                      "of a (32, 1024^3) f32 series, (4, 256^3) chunks, r=2" % rank,
+            "groups_t_z": list(groups), "output_box": [list(a.out_start), list(a.out_shape)],
+            "input_box": [list(a.in_start), list(a.in_shape)], "ms": round(ms, 4),
+            "value": round(n * 4 / 2 ** 30 / (ms / 1e3), 3), "unit": "GiB/s",
+            "projected_8gpu_gibs": round(8 * n * 4 / 2 ** 30 / (ms / 1e3), 3),
+            "roofline": _roof(n * ALGO_BYTES_PER_VOXEL, ms, load_leg_traffic("t_share")),
+            "parity": {"max_rel": float(f"{worst:.3e}"), "tol": FLOAT_TOL,
+                       "ok": worst <= FLOAT_TOL, "boxes": [list(c) for c in starts],
+                       "box_shape": list(box)}}
+
+
+def leg_pyramid_octant(ctx, L, stream, warmup, reps):
+    """configs[3] per GPU: one rank's level-0 octant (2048^3 of the 4096^3 u16 volume) of the
+    8-GPU zarrs_ome split, factor 2, 5 levels, the level-fused device pyramid."""
+    import numpy as np
+    import torch
+    import zarrs_tools_amd as zt
+    from oracle import oracle as O
+    gshape, n, levels = (4096,) * 3, 2048, 5
+    x = zt.synth_box((0, 0, 0), (n,) * 3, gshape, kind="uint16", ctx=ctx)
+    res = {}
+
+    def step():
+        res["lv"] = None
+        res["lv"] = zt.pyramid(x, (2, 2, 2), levels, ctx=ctx)
+    ms = _time_ms(step, stream, warmup, reps)
+    lv = res.pop("lv")
+    nbytes = 2 * n ** 3 + sum(2 * int(np.prod(t.shape)) for t in lv)
+    # parity (bit-exact): 64^3 level-0 blocks aligned to 2^5, their 5 levels from the oracle
+    worst_ok = True
+    starts = [(0, 0, 0), (n - 64,) * 3, (1024, 512, 1536)]
+    for st in starts:
+        cur = O.synth_block_nd(st, (64,) * 3, gshape, "uint16")
+        for k, t in enumerate(lv):
+            cur = O.downsample(cur, "uint16", (2, 2, 2), "uint16")
+            f = 2 ** (k + 1)
+            sl = tuple(slice(a // f, a // f + c) for a, c in zip(st, cur.shape))
+            got = t[sl].cpu().numpy()
+            worst_ok = worst_ok and np.array_equal(got, cur)
+    del x, lv
+    torch.cuda.empty_cache()
+    return {"config": "BASELINE configs[3] per GPU: the level-0 octant 2048^3 of the 4096^3 "
+                      "u16 volume, factor 2, 5 levels (zarrs_ome device pyramid)",
+            "ms": round(ms, 4), "input_gvox_per_s": round(n ** 3 / (ms / 1e3) / 1e9, 3),
+            "roofline": _roof(nbytes, ms, load_leg_traffic("pyramid_octant")),
+            "parity": {"bit_exact": bool(worst_ok), "blocks": [list(s) for s in starts],
+                       "block_shape": [64] * 3, "levels": levels}}
+
+
+def leg_gaussian(ctx, L, stream, warmup, reps):
+    """zarrs_filter gaussian sigma 1,1,1 half 3,3,3 on 1024^3 f32 (256^3 chunks)."""
+    import numpy as np
+    import torch
+    import zarrs_tools_amd as zt
+    from oracle import oracle as O
+    n = 1024
+    x = zt.synth_step_noise_f32((n,) * 3, ctx=ctx)
+    y = torch.empty_like(x)
+    g = zt.Gaussian([1.0] * 3, [3] * 3)
+    a_in, a_out = zt.DeviceArray(x, (CHUNK,) * 3), zt.DeviceArray(y, (CHUNK,) * 3)
+    ms = _time_ms(lambda: g.apply(a_in, a_out, ctx=ctx), stream, warmup, reps)
+    # parity (bit-exact): 32^3 output boxes from the oracle on the box + its 3-voxel halo
+    ok = True
+    starts = [(0, 0, 0), (n - 32,) * 3, (500, 257, 640)]
+    for st in starts:
+        i0 = tuple(max(0, a - 3) for a in st)
+        i1 = tuple(min(n, a + 32 + 3) for a in st)
+        blk = O.synth_block_nd(i0, tuple(b - a for a, b in zip(i0, i1)), (n,) * 3, "float32")
+        ref = O.gaussian_apply_ndarray(blk, [1.0] * 3, [3] * 3)
+        sl = tuple(slice(a - b, a - b + 32) for a, b in zip(st, i0))
+        got = y[tuple(slice(a, a + 32) for a in st)].cpu().numpy()
+        ok = ok and np.array_equal(got, ref[sl])
+    del x, y
+    torch.cuda.empty_cache()
+    return {"config": "gaussian sigma 1,1,1 half 3,3,3 on 1024^3 f32, 256^3 chunks (zarrs_filter "
+                      "gaussian, SURVEY.md §8 (f)3)", "ms": round(ms, 4),
+            "value": round(n ** 3 * 4 / 2 ** 30 / (ms / 1e3), 3), "unit": "GiB/s",
+            "roofline": _roof(n ** 3 * 8, ms, load_leg_traffic("gaussian")),
+            "parity": {"bit_exact": bool(ok), "boxes": [list(s) for s in starts],
+                       "box_shape": [32] * 3}}
+
+
+EXTRA_LEGS = {"g2": leg_g2, "t_share": leg_t_share, "pyramid_octant": leg_pyramid_octant,
+              "gaussian": leg_gaussian}
 
 
 def main():
@@ -337,6 +568,18 @@ def main():
     if rank == 0 and args.parity_chunks > 0:
         res["parity"] = parity_sample(out, a, gshape, radius, args.parity_chunks)
         res["parity_max_rel"] = res["parity"]["max_rel"]
+    if world == 1 and share is None and not args.no_extra and headline:
+        del slab, out
+        torch.cuda.empty_cache()
+        extra = {}
+        for name in [n for n in args.extra.split(",") if n]:
+            try:
+                t0 = time.perf_counter()
+                extra[name] = EXTRA_LEGS[name](ctx, L, stream, 1, max(3, min(args.steps, 10)))
+                extra[name]["wall_s"] = round(time.perf_counter() - t0, 2)
+            except Exception as e:  # reported, never fatal to the headline line
+                extra[name] = {"error": f"{type(e).__name__}: {e}"}
+        res["extra_configs"] = extra
     if rank == 0:
         print(json.dumps(res), flush=True)
     ctx.close()

@@ -23,9 +23,13 @@ def _level_u16_2x(x):
     return O.downsample(np.asarray(x), "uint16", (2, 2, 2), "uint16")
 
 
-@pytest.mark.parametrize("world,prespawn", [(2, False), (3, False), (4, False), (2, True)])
-def test_octant_processes_assemble_the_global_pyramid(tmp_path, world, prespawn):
-    shape, chunk, factor = (64, 48, 80), (16, 16, 16), (2, 2, 2)
+@pytest.mark.parametrize("world,prespawn,shape", [
+    (2, False, (64, 48, 80)), (3, False, (64, 48, 80)), (4, False, (64, 48, 80)),
+    (2, True, (64, 48, 80)),
+    # config P's split on an 8-GPU node: 8 octants (2 x 2 x 2 rank grid), warmed-up workers
+    (8, True, (64, 64, 96))])
+def test_octant_processes_assemble_the_global_pyramid(tmp_path, world, prespawn, shape):
+    chunk, factor = (16, 16, 16), (2, 2, 2)
     u = O.synth_u16(shape)
     S.create_array(tmp_path / "in.zarr", "uint16", shape, chunk)
     S.write_array(tmp_path / "in.zarr", u)
@@ -47,6 +51,9 @@ def test_octant_processes_assemble_the_global_pyramid(tmp_path, world, prespawn)
             pool.shutdown()
     assert done == L
     assert st["assembled_chunks"] > 0  # the upper levels cross box boundaries
+    assert st["processes"] == world
+    if world == 8:
+        assert list(st["grid"]) == [2, 2, 2]
     want = u
     for k in range(1, L + 1):
         want = _level_u16_2x(want)

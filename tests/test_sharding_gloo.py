@@ -193,3 +193,58 @@ def test_octant_split_gloo_world2_equals_whole_pyramid():
     want = _oracle_levels(O.synth_u16((48, 40, 72)), (2, 2, 2), len(levels))
     for g, w in zip(levels, want):
         np.testing.assert_array_equal(g, w)
+
+
+# ---- world size 8: the two splits an 8-GPU node runs -------------------------------------------
+SHAPE_T = (16, 32, 5, 6)     # (t, z, y, x): 8 t-chunks x 4 z-chunks (config T: 8 x 4)
+CHUNK_T = (2, 8, 5, 6)
+R_T = 1
+
+
+def _tz_worker(rank, world, port, q):
+    """Config T's (t, z) block split (shard.block_split / block_assignment, the split
+    zarrs_filter --gpus 8 and bench.py's T-share leg use): this rank filters its halo'd input box
+    on its output box only (the oracle standing in for the device path), the boxes are gathered
+    over gloo (the test's checker; the real path has no collective)."""
+    from zarrs_tools_amd import shard
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        groups = shard.block_split(world, SHAPE_T, CHUNK_T, 2 * R_T)
+        a = shard.block_assignment(rank, world, SHAPE_T, CHUNK_T, 2 * R_T, groups)
+        mine = np.zeros(SHAPE_T, np.float32)
+        cover = np.zeros(SHAPE_T[:2], np.int64)
+        if int(np.prod(a.out_shape)):
+            blk = O.synth_block_nd(a.in_start, a.in_shape, SHAPE_T, "float32")
+            res = O.guided_filter_apply_ndarray(blk, EPS, R_T)
+            src = tuple(slice(o - i, o - i + s) for o, i, s in zip(a.out_start, a.in_start,
+                                                                 a.out_shape))
+            dst = tuple(slice(o, o + s) for o, s in zip(a.out_start, a.out_shape))
+            mine[dst] = res[src]
+            cover[dst[:2]] += 1
+        t, c = torch.from_numpy(mine), torch.from_numpy(cover)
+        dist.all_reduce(t)
+        dist.all_reduce(c)
+        if rank == 0:
+            q.put((t.numpy(), c.numpy(), tuple(groups)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_tz_block_split_world8_equals_whole_series():
+    world = 8
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_tz_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got, cover, groups = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert groups == (2, 4)  # config T's split: 2 t-groups x 4 z-groups
+    assert (cover == 1).all()
+    whole = O.guided_filter_apply(O.synth_step_noise_f32(SHAPE_T), CHUNK_T, EPS, R_T, nthreads=4)
+    assert np.abs(got - whole).max() <= 1e-5 * np.abs(whole).max()

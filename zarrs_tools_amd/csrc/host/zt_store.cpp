@@ -1104,15 +1104,16 @@ int zt_store_guided_filter_box(const char* in_path, const char* out_path, int dt
         const int din = in.dtype;
         int64_t plane = 1;
         for (int d = 1; d < nd; ++d) plane *= shape[d];
-        op.scratch_bytes = [&](int64_t planes) -> uint64_t {
-            // separable path (n-D or r > 8): 5 f32 words per slab voxel; fused path: f32 staging
-            // of non-direct element types
-            return (uint64_t)planes * plane * ((nd == 3 && radius <= 8) ? 8 : 20);
-        };
         // an output window of chunk columns along axis 1 (config T's (t, z) blocks,
         // shard.block_assignment): its input carries the halo along axis 1 too
         ColWin win{};
         const bool windowed = nd >= 2 && col_end >= 0;
+        op.scratch_bytes = [&, windowed](int64_t planes) -> uint64_t {
+            // separable path (n-D, r > 8, or a column window, which apply takes through
+            // apply_ndarray's separable form): 5 f32 words per slab voxel; fused path: f32
+            // staging of non-direct element types
+            return (uint64_t)planes * plane * ((nd == 3 && radius <= 8 && !windowed) ? 8 : 20);
+        };
         if (windowed) {
             const int64_t oc = out.chunk_shape[1], n1 = in.shape[1];
             const int64_t ncol = (out.shape[1] + oc - 1) / oc;

@@ -313,6 +313,9 @@ def read_to_device(path, device: int, nthreads: int = 0, start=None, shape=None)
         bufs = [torch.empty((n_max,), dtype=tdt, pin_memory=True) for _ in range(nbuf)]
         evs = [None] * nbuf
         stream = torch.cuda.Stream(device=dev)
+        # x was allocated on the caller's current stream: order the copies after any work that
+        # stream still has queued on the block the caching allocator handed back
+        stream.wait_stream(torch.cuda.current_stream(dev))
 
         def decode(k):
             a, b, ya, yb = pieces[k]

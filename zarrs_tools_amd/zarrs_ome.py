@@ -457,27 +457,45 @@ def _octant_warmup(device: int) -> float:
     return time.time()
 
 
-def octant_pool(gpus: int, devices):
-    """The spawned process pool of run_octants, started early with a warm-up task per process,
-    before this process initialises any device (spawn, not fork)."""
-    import multiprocessing as mp
-    from concurrent.futures import ProcessPoolExecutor
-    ex = ProcessPoolExecutor(gpus, mp_context=mp.get_context("spawn"))
-    # the workers never import torch (ZT_NO_TORCH=1 in the environment they are spawned with:
-    # processes start at submit, one per warm-up task; with no warm-up they start at the first
-    # task, inside the same setting)
-    old = os.environ.get("ZT_NO_TORCH")
-    if os.environ.get("ZT_OCTANT_TORCH") != "1":  # (=1: torch workers, for A/B runs)
-        os.environ["ZT_NO_TORCH"] = "1"
-    try:
-        for d in list(devices)[:gpus]:
-            ex.submit(_octant_warmup, d)
-    finally:
-        if old is None:
-            os.environ.pop("ZT_NO_TORCH", None)
-        else:
-            os.environ["ZT_NO_TORCH"] = old
-    return ex
+class OctantPool:
+    """The spawned worker processes of run_octants: one single-process executor per rank, warmed
+    up on that rank's device, so the rank's octant task runs in the process whose HIP context
+    already lives on its device (a shared queue could hand a warmed worker another device's task
+    and leave contexts on two devices)."""
+
+    def __init__(self, devices):
+        import multiprocessing as mp
+        from concurrent.futures import ProcessPoolExecutor
+        ctx = mp.get_context("spawn")
+        self.devices = list(devices)
+        self.execs = [ProcessPoolExecutor(1, mp_context=ctx) for _ in self.devices]
+        # the workers never import torch (ZT_NO_TORCH=1 in the environment they are spawned with:
+        # a process starts at its first submit, the warm-up, inside this setting)
+        old = os.environ.get("ZT_NO_TORCH")
+        if os.environ.get("ZT_OCTANT_TORCH") != "1":  # (=1: torch workers, for A/B runs)
+            os.environ["ZT_NO_TORCH"] = "1"
+        try:
+            for ex, d in zip(self.execs, self.devices):
+                ex.submit(_octant_warmup, d)
+        finally:
+            if old is None:
+                os.environ.pop("ZT_NO_TORCH", None)
+            else:
+                os.environ["ZT_NO_TORCH"] = old
+
+    def submit(self, rank: int, fn, *args):
+        """Run fn(*args) in rank's process (rank's device was warmed up there)."""
+        return self.execs[rank].submit(fn, *args)
+
+    def shutdown(self, wait: bool = True, cancel_futures: bool = False) -> None:
+        for ex in self.execs:
+            ex.shutdown(wait=wait, cancel_futures=cancel_futures)
+
+
+def octant_pool(gpus: int, devices) -> OctantPool:
+    """The worker processes of run_octants, started early with a warm-up task each (rank g on
+    devices[g]), before this process initialises any device (spawn, not fork)."""
+    return OctantPool(list(devices)[:gpus])
 
 
 def run_octants(out_root: str, shape0, factor, levels, discrete: bool, gpus: int, devices=None,
@@ -500,7 +518,7 @@ def run_octants(out_root: str, shape0, factor, levels, discrete: bool, gpus: int
     ex = pool if pool is not None else octant_pool(gpus, devices)
     try:
         try:
-            futs = [ex.submit(_octant_worker, out_root, assigns[g], list(factor), discrete,
+            futs = [ex.submit(g, _octant_worker, out_root, assigns[g], list(factor), discrete,
                               devices[g], per, scratch, envs[g], compute, src0)
                     for g in range(gpus) if assigns[g].coord is not None]
             parts = [f.result() for f in futs]
@@ -607,6 +625,8 @@ def _run(input_path, output_path, info, nd, factor, max_levels, discrete, name, 
         if all(f == 1 or s == 1 for f, s in zip(factor, cur_shape)):
             break
     multi = gpus > 1 and _device_ok(device)
+    if pool is not None and not (multi and level_shapes):
+        pool.shutdown(wait=True, cancel_futures=True)  # no octant path: release the workers
     dt0 = (reencoding or {}).get("data_type") or info.data_type
     info0 = S.ArrayInfo(lvl0, dt0, tuple(info.shape), info.chunk_shape, info.inner_chunk_shape)
     on_device = (not multi and device_resident and _device_ok(device)
@@ -651,6 +671,10 @@ def _run(input_path, output_path, info, nd, factor, max_levels, discrete, name, 
         fits = all(_device_pyramid_fits(box_info, None, d, sharing=devices.count(d),
                                         host_share=gpus) for d in sorted(set(devices)))
         phases["octant_checks_done"] = time.perf_counter() - t0
+        if not (big.local_levels > 0 and fits) and pool is not None:
+            # the octant path is not taken: release the warmed-up workers (and their device
+            # contexts) before the row-split processes start
+            pool.shutdown(wait=True, cancel_futures=True)
         if big.local_levels > 0 and fits:
             prepare_octant_levels(output_path, level_shapes, big.local_levels, src0)
             octants_done, st_oct = run_octants(output_path, list(info.shape), factor,
