@@ -63,6 +63,9 @@ def parse():
                          "config-T share, the config-P octant pyramid, the Gaussian)")
     ap.add_argument("--extra", default="g2,t_share,pyramid_octant,gaussian",
                     help="comma list of the extra legs to run")
+    ap.add_argument("--only-extra", default=None, metavar="LEG",
+                    help="run only this extra leg, one untimed-warmup-free call (PMC passes: "
+                         "tools/profile_pmc_legs.sh)")
     return ap.parse_args()
 
 
@@ -468,6 +471,12 @@ def main():
         a = zt.slab_assignment(rank, world, gshape[0], CHUNK, 2 * radius)
     stream = torch.cuda.current_stream(dev)
     ctx = zt.Context(local, stream)
+    if args.only_extra:  # one call of one extra leg (its PMC passes); no headline
+        L = _abi.lib()
+        r = EXTRA_LEGS[args.only_extra](ctx, L, stream, 0, 1)
+        print(json.dumps({"leg": args.only_extra, **r}), flush=True)
+        ctx.close()
+        return
 
     slab = torch.empty((a.in_nz, size, size), dtype=torch.float32, device=dev)
     out = torch.empty((a.out_nz, size, size), dtype=torch.float32, device=dev)

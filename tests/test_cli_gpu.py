@@ -282,12 +282,16 @@ def test_store_step_split_over_processes_equals_one_process(tmp_path):
 
 
 @pytest.mark.parametrize("gpus,mode", [(2, "mean"), (4, "mean"), (3, "discrete"),
-                                       (2, "gaussian")])
-def test_zarrs_ome_gpus_split_equals_one_process(tmp_path, gpus, mode):
+                                       (2, "gaussian"), (2, "mean_pieces")])
+def test_zarrs_ome_gpus_split_equals_one_process(tmp_path, gpus, mode, monkeypatch):
     """zarrs_ome --gpus N (rehearsed with every process on device 0): octant-owned levels with
     host assembly of boundary chunks (mean / mode), or every level split by chunk rows
     (--gaussian-sigma), give the one-process levels, level metadata and group metadata bit for
-    bit."""
+    bit. mean_pieces: 1 KiB read pieces (ZT_READ_PIECE_KB=1, inherited by the spawned workers),
+    so the torch-free workers' box reads take the pitched hipMemcpy2DAsync sub-row copies."""
+    if mode == "mean_pieces":
+        monkeypatch.setenv("ZT_READ_PIECE_KB", "1")
+        mode = "mean"
     shape, chunk = (64, 48, 80), (16, 16, 16)
     u = O.synth_u16(shape)
     S.create_array(tmp_path / "in.zarr", "uint16", shape, chunk)

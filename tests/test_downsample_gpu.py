@@ -114,13 +114,53 @@ def test_fused_pyramid_levels_equal_per_level_launches(shape, dtype, monkeypatch
         v = rng.integers(info.min, info.max, shape, dtype=dtype, endpoint=True)
     x = to_dev(v, dtype)
     levels = zt.pyramid(x, (2, 2, 2), max_levels=6)
-    monkeypatch.setenv("ZT_PYRAMID_UNFUSED", "1")
-    plain = zt.pyramid(x, (2, 2, 2), max_levels=6)
+    # the per-level launches: one Downsample::apply_ndarray_continuous per level
+    plain, cur_dev = [], x
+    for _ in levels:
+        cur_dev = zt.Downsample((2, 2, 2)).apply_ndarray_continuous(cur_dev)
+        plain.append(cur_dev)
     torch.cuda.synchronize()
-    assert len(levels) == len(plain) == len(zt.pyramid_level_shapes(shape, (2, 2, 2), 6))
+    assert len(levels) == len(zt.pyramid_level_shapes(shape, (2, 2, 2), 6))
     cur = v
     for got, ref in zip(levels, plain):
         cur = O.downsample(cur, dtype, (2, 2, 2), dtype)
+        g = from_dev(got, dtype)
+        assert g.shape == cur.shape
+        np.testing.assert_array_equal(g, cur)
+        np.testing.assert_array_equal(g, from_dev(ref, dtype))
+
+
+@pytest.mark.parametrize("shape,dtype,levels", [
+    ((37, 50, 71), "uint16", 6), ((64, 64, 64), "uint8", 6), ((9, 17, 33), "int16", 6),
+    ((19, 32, 40), "int64", 6), ((16, 16, 264), "uint32", 6), ((70, 8, 8), "int8", 6),
+    ((33, 34, 35), "bool", 6), ((40, 36, 72), "int32", 2)])
+def test_fused_mode_pyramid_equals_oracle_levels(shape, dtype, levels):
+    """zarrs_ome --discrete on the device: the level-fused mode pyramid (pyr_mode8, up to three
+    levels per launch) gives, level by level, the oracle's discrete downsample of the previous
+    level (the most frequent value, ties to the smallest: the documented tie rule) and the
+    per-level mode launches. Few distinct values so that ties and majorities both occur."""
+    import torch
+    rng = np.random.default_rng(sum(shape) + levels)
+    if dtype == "bool":
+        v = rng.integers(0, 2, shape).astype(bool)
+    else:
+        info = np.iinfo(dtype)
+        # (the oracle compares window values as f64: 64-bit values within 2^52 stay exact)
+        lo, hi = (max(info.min, -2 ** 52), min(info.max, 2 ** 52)) if info.bits == 64 \
+            else (info.min, info.max)
+        pool = rng.integers(lo, hi, 5, dtype=dtype, endpoint=True)
+        v = pool[rng.integers(0, 5, shape)]
+    x = to_dev(v, dtype)
+    got_levels = zt.pyramid(x, (2, 2, 2), max_levels=levels, discrete=True)
+    plain, cur_dev = [], x
+    for _ in got_levels:
+        cur_dev = zt.Downsample((2, 2, 2), discrete=True).apply_ndarray_discrete(cur_dev)
+        plain.append(cur_dev)
+    torch.cuda.synchronize()
+    assert len(got_levels) == len(zt.pyramid_level_shapes(shape, (2, 2, 2), levels))
+    cur = v
+    for got, ref in zip(got_levels, plain):
+        cur = O.downsample(cur, dtype, (2, 2, 2), dtype, discrete=True)
         g = from_dev(got, dtype)
         assert g.shape == cur.shape
         np.testing.assert_array_equal(g, cur)

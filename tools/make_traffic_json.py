@@ -5,6 +5,7 @@ the workload and the world size, so bench.py only reports it for the build it wa
 
 Usage: make_traffic_json.py PMC_DIR OUT_JSON [size radius [G/N]]  (merges into OUT_JSON's entries;
 G/N keys the entry to a `bench.py --share G/N` proxy run)
+       make_traffic_json.py --legs PMC_DIR OUT_JSON [legs...]  (bench.py's extra legs)
 Method (MI355X_MICROARCH.md, HBM / rocprofv3): one launch (bench.py --steps 1 --warmup 0), each
 counter in its own run; FETCH_SIZE and WRITE_SIZE are KiB; FETCH_SIZE x2 is the gfx950
 correction for wide (128 B) reads counted as 64 B.
@@ -29,7 +30,59 @@ def total(d, counter, pat="gf3d"):
     return v, len(n)
 
 
+def lib_sha() -> str:
+    h = hashlib.sha256()
+    with open(os.path.join(ROOT, "zarrs_tools_amd", "libzarrs_tools_amd.so"), "rb") as f:
+        for blk in iter(lambda: f.read(1 << 20), b""):
+            h.update(blk)
+    return h.hexdigest()
+
+
+def merge(out, keep, d):
+    entries = []
+    if os.path.exists(out):
+        try:
+            old = json.load(open(out))
+            entries = old.get("entries", [old]) if isinstance(old, dict) else list(old)
+        except ValueError:
+            entries = []
+    entries = [e for e in entries if e.get("lib_sha256") == d["lib_sha256"] and keep(e)]
+    entries.append(d)
+    with open(out, "w") as f:
+        json.dump({"entries": entries}, f, indent=1)
+    print(json.dumps(d))
+
+
+def legs_main(pmc, out, legs):
+    """Entries for bench.py's extra legs from tools/profile_pmc_legs.sh: every kernel of one
+    call (bench.py --only-extra LEG) except the synthetic-input generators."""
+    sha = lib_sha()
+    for leg in legs:
+        rd = wr = 0.0
+        names = set()
+        for c, dst in (("FETCH_SIZE", "r"), ("WRITE_SIZE", "w")):
+            for f in glob.glob(os.path.join(pmc, f"{leg}_{c}", "**", "run_counter_collection.csv"),
+                               recursive=True):
+                for r in csv.DictReader(open(f)):
+                    if r["Counter_Name"] != c or "synth" in r["Kernel_Name"]:
+                        continue
+                    names.add(r["Kernel_Name"].split("(")[0][:80])
+                    if dst == "r":
+                        rd += float(r["Counter_Value"]) * 1024 * 2
+                    else:
+                        wr += float(r["Counter_Value"]) * 1024
+        d = {"lib_sha256": sha, "leg": leg, "hbm_bytes_per_call": rd + wr, "read_bytes": rd,
+             "write_bytes": wr, "kernels": sorted(names),
+             "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate runs of "
+                       "bench.py --only-extra LEG (one call); FETCH_SIZE x2 (gfx950 wide-read "
+                       "correction), KiB -> bytes; synthetic-input kernels excluded"}
+        merge(out, lambda e, leg=leg: e.get("leg") != leg, d)
+
+
 def main():
+    if sys.argv[1] == "--legs":
+        return legs_main(sys.argv[2], sys.argv[3], sys.argv[4:] or
+                         ["g2", "t_share", "pyramid_octant", "gaussian"])
     pmc, out = sys.argv[1], sys.argv[2]
     size = int(sys.argv[3]) if len(sys.argv) > 3 else 2048
     radius = int(sys.argv[4]) if len(sys.argv) > 4 else 4

@@ -118,7 +118,8 @@ __global__ __launch_bounds__(256) void downsample_discrete_kernel(const TIn* __r
 // ---------------------------------------------------------------------------------------------
 // Fused 2x2x2 mean pyramid: NL = 2 or 3 levels of zarrs_ome's loop (zarrs_ome.rs:515-738, each
 // level downsample.rs:72-97 of the previous one) in one launch, so the intermediate levels are
-// written once and never read back. Every output is computed exactly as downsample3_kernel does
+// written once and never read back. MODE: the same with the mode of each window (zarrs_ome
+// --discrete, downsample.rs:99-120; pyr_mode8), each level the mode of the previous level. Every output is computed exactly as downsample3_kernel does
 // it (C-order f64 sum from -0.0 of the previous level's `as`-rounded values, / 8, `as T`; 8- to
 // 32-bit integers summed exactly in integers, the same value), so the levels are bit-identical
 // to per-level launches.
@@ -156,7 +157,40 @@ __device__ __forceinline__ T pyr_mean8(const T (&v)[8]) {  // v in C order of th
     }
 }
 
-template <typename T, int NL, bool VEC>
+// Mode of a 2x2x2 window (downsample.rs:99-120): the most frequent value, ties to the smallest
+// (the reference's HashMap order is unspecified). 28 pairwise compares in
+// registers; the same value the per-level kernels and the oracle pick.
+template <typename T>
+__device__ __forceinline__ T pyr_mode8(const T (&v)[8]) {
+    int c[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) c[i] = 1;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = i + 1; j < 8; ++j) {
+            const int e = v[i] == v[j];
+            c[i] += e;
+            c[j] += e;
+        }
+    T best = v[0];
+    int bc = c[0];
+#pragma unroll
+    for (int i = 1; i < 8; ++i)
+        if (c[i] > bc || (c[i] == bc && v[i] < best)) {
+            best = v[i];
+            bc = c[i];
+        }
+    return best;
+}
+
+template <typename T, bool MODE>
+__device__ __forceinline__ T pyr_reduce8(const T (&v)[8]) {
+    if constexpr (MODE) return pyr_mode8<T>(v);
+    else return pyr_mean8<T>(v);
+}
+
+template <typename T, int NL, bool VEC, bool MODE = false>
 __global__ __launch_bounds__(256) void pyramid3_fused_kernel(const T* __restrict__ in,
                                                              T* __restrict__ l1,
                                                              T* __restrict__ l2,
@@ -204,7 +238,7 @@ __global__ __launch_bounds__(256) void pyramid3_fused_kernel(const T* __restrict
                                     v[2 * i + 1][2 * j][2 * k], v[2 * i + 1][2 * j][2 * k + 1],
                                     v[2 * i + 1][2 * j + 1][2 * k],
                                     v[2 * i + 1][2 * j + 1][2 * k + 1]};
-                    u1[i][j][k] = pyr_mean8<T>(t);
+                    u1[i][j][k] = pyr_reduce8<T, MODE>(t);
                 }
         const int64_t z1b = 4 * bz + 2 * dz, y1b = 4 * by + 2 * dy, x1b = 4 * x3;
 #pragma unroll
@@ -233,7 +267,7 @@ __global__ __launch_bounds__(256) void pyramid3_fused_kernel(const T* __restrict
             const T t[8] = {u1[0][0][2 * m], u1[0][0][2 * m + 1], u1[0][1][2 * m],
                             u1[0][1][2 * m + 1], u1[1][0][2 * m], u1[1][0][2 * m + 1],
                             u1[1][1][2 * m], u1[1][1][2 * m + 1]};
-            u2[m] = pyr_mean8<T>(t);
+            u2[m] = pyr_reduce8<T, MODE>(t);
         }
         const int64_t z2 = 2 * bz + dz, y2 = 2 * by + dy, x2 = 2 * x3;
         if (z2 < n2z && y2 < n2y) {
@@ -249,7 +283,7 @@ __global__ __launch_bounds__(256) void pyramid3_fused_kernel(const T* __restrict
                 const T t[8] = {lds2[0][lane][0], lds2[0][lane][1], lds2[1][lane][0],
                                 lds2[1][lane][1], lds2[2][lane][0], lds2[2][lane][1],
                                 lds2[3][lane][0], lds2[3][lane][1]};
-                const T u3 = pyr_mean8<T>(t);
+                const T u3 = pyr_reduce8<T, MODE>(t);
                 if (bz < p.s[3][0] && by < p.s[3][1] && x3 < p.s[3][2])
                     l3[(bz * p.s[3][1] + by) * p.s[3][2] + x3] = u3;
             }
@@ -258,7 +292,7 @@ __global__ __launch_bounds__(256) void pyramid3_fused_kernel(const T* __restrict
     }
 }
 
-template <typename T>
+template <typename T, bool MODE>
 static hipError_t launch_pyr_fused_t(const void* in, void* const* outs, const PyrParams& p,
                                      int nl, hipStream_t s) {
     const int64_t gx = (p.s[1][2] + 255) / 256, gy = (p.s[1][1] + 3) / 4;
@@ -274,40 +308,77 @@ static hipError_t launch_pyr_fused_t(const void* in, void* const* outs, const Py
     T* o2 = static_cast<T*>(outs[1]);
     T* o3 = nl == 3 ? static_cast<T*>(outs[2]) : nullptr;
     if (nl == 3) {
-        if (vec) hipLaunchKernelGGL((pyramid3_fused_kernel<T, 3, true>), grid, dim3(256), 0, s, i, o1, o2, o3, p);
-        else hipLaunchKernelGGL((pyramid3_fused_kernel<T, 3, false>), grid, dim3(256), 0, s, i, o1, o2, o3, p);
+        if (vec) hipLaunchKernelGGL((pyramid3_fused_kernel<T, 3, true, MODE>), grid, dim3(256), 0, s, i, o1, o2, o3, p);
+        else hipLaunchKernelGGL((pyramid3_fused_kernel<T, 3, false, MODE>), grid, dim3(256), 0, s, i, o1, o2, o3, p);
     } else {
-        if (vec) hipLaunchKernelGGL((pyramid3_fused_kernel<T, 2, true>), grid, dim3(256), 0, s, i, o1, o2, o3, p);
-        else hipLaunchKernelGGL((pyramid3_fused_kernel<T, 2, false>), grid, dim3(256), 0, s, i, o1, o2, o3, p);
+        if (vec) hipLaunchKernelGGL((pyramid3_fused_kernel<T, 2, true, MODE>), grid, dim3(256), 0, s, i, o1, o2, o3, p);
+        else hipLaunchKernelGGL((pyramid3_fused_kernel<T, 2, false, MODE>), grid, dim3(256), 0, s, i, o1, o2, o3, p);
     }
     return hipGetLastError();
+}
+
+// 3-D 2x2x2 mode (downsample.rs:99-120) for the per-level launches: one output per thread on an
+// (x, y, z) grid (no 64-bit index divisions, unlike the N-d kernel), the window's 8 values in
+// registers (pyr_mode8).
+template <typename TIn, typename TOut>
+__global__ __launch_bounds__(256) void downsample3_mode_kernel(const TIn* __restrict__ in,
+                                                               TOut* __restrict__ out,
+                                                               DSParams p) {
+    const int64_t onx = p.out_shape[2], ony = p.out_shape[1], onz = p.out_shape[0];
+    const int64_t inx = p.in_shape[2], iny = p.in_shape[1];
+    const int64_t x = (int64_t)blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
+    if (x >= onx) return;
+    for (int64_t z = blockIdx.z; z < onz; z += gridDim.z) {
+        const TIn* src = in + ((z * 2) * iny + y * 2) * inx + x * 2;
+        const TIn t[8] = {src[0], src[1], src[inx], src[inx + 1], src[iny * inx],
+                          src[iny * inx + 1], src[(iny + 1) * inx], src[(iny + 1) * inx + 1]};
+        const TIn best = pyr_mode8<TIn>(t);
+        if constexpr (std::is_integral<TOut>::value) out[(z * ony + y) * onx + x] = (TOut)best;
+        else out[(z * ony + y) * onx + x] = from_f64<TOut>((double)best);
+    }
 }
 
 bool pyramid_fused_grid_fits(const int64_t* s1) {
     return (s1[2] + 255) / 256 <= 0x7FFFFFFF && (s1[1] + 3) / 4 <= 65535;
 }
 
-bool pyramid_fused_dtype(int dtype) {
+bool pyramid_fused_dtype(int dtype, bool discrete) {
+    if (discrete)  // the mode needs Eq + Hash element types (downsample.rs:105): integers, bool
+        return dtype == kBool || dtype == kU8 || dtype == kI8 || dtype == kU16 || dtype == kI16 ||
+               dtype == kU32 || dtype == kI32 || dtype == kU64 || dtype == kI64;
     return dtype != kBF16 && dtype != kF16 && dtype_size(dtype) > 0;
 }
 
 hipError_t launch_pyramid_fused(const void* in, int dtype, const int64_t (*shapes)[3], int nl,
-                                void* const* outs, hipStream_t s) {
+                                void* const* outs, bool discrete, hipStream_t s) {
     if (nl != 2 && nl != 3) return hipErrorInvalidValue;
     PyrParams p{};
     for (int l = 0; l <= nl; ++l)
         for (int d = 0; d < 3; ++d) p.s[l][d] = shapes[l][d];
+    if (discrete) {
+        switch (dtype) {
+        case kBool: case kU8: return launch_pyr_fused_t<uint8_t, true>(in, outs, p, nl, s);
+        case kI8: return launch_pyr_fused_t<int8_t, true>(in, outs, p, nl, s);
+        case kI16: return launch_pyr_fused_t<int16_t, true>(in, outs, p, nl, s);
+        case kU16: return launch_pyr_fused_t<uint16_t, true>(in, outs, p, nl, s);
+        case kI32: return launch_pyr_fused_t<int32_t, true>(in, outs, p, nl, s);
+        case kU32: return launch_pyr_fused_t<uint32_t, true>(in, outs, p, nl, s);
+        case kI64: return launch_pyr_fused_t<int64_t, true>(in, outs, p, nl, s);
+        case kU64: return launch_pyr_fused_t<uint64_t, true>(in, outs, p, nl, s);
+        default: return hipErrorInvalidValue;
+        }
+    }
     switch (dtype) {
-    case kBool: case kU8: return launch_pyr_fused_t<uint8_t>(in, outs, p, nl, s);
-    case kI8: return launch_pyr_fused_t<int8_t>(in, outs, p, nl, s);
-    case kI16: return launch_pyr_fused_t<int16_t>(in, outs, p, nl, s);
-    case kU16: return launch_pyr_fused_t<uint16_t>(in, outs, p, nl, s);
-    case kI32: return launch_pyr_fused_t<int32_t>(in, outs, p, nl, s);
-    case kU32: return launch_pyr_fused_t<uint32_t>(in, outs, p, nl, s);
-    case kI64: return launch_pyr_fused_t<int64_t>(in, outs, p, nl, s);
-    case kU64: return launch_pyr_fused_t<uint64_t>(in, outs, p, nl, s);
-    case kF32: return launch_pyr_fused_t<float>(in, outs, p, nl, s);
-    case kF64: return launch_pyr_fused_t<double>(in, outs, p, nl, s);
+    case kBool: case kU8: return launch_pyr_fused_t<uint8_t, false>(in, outs, p, nl, s);
+    case kI8: return launch_pyr_fused_t<int8_t, false>(in, outs, p, nl, s);
+    case kI16: return launch_pyr_fused_t<int16_t, false>(in, outs, p, nl, s);
+    case kU16: return launch_pyr_fused_t<uint16_t, false>(in, outs, p, nl, s);
+    case kI32: return launch_pyr_fused_t<int32_t, false>(in, outs, p, nl, s);
+    case kU32: return launch_pyr_fused_t<uint32_t, false>(in, outs, p, nl, s);
+    case kI64: return launch_pyr_fused_t<int64_t, false>(in, outs, p, nl, s);
+    case kU64: return launch_pyr_fused_t<uint64_t, false>(in, outs, p, nl, s);
+    case kF32: return launch_pyr_fused_t<float, false>(in, outs, p, nl, s);
+    case kF64: return launch_pyr_fused_t<double, false>(in, outs, p, nl, s);
     default: return hipErrorInvalidValue;
     }
 }
@@ -321,8 +392,18 @@ static hipError_t launch_ds_types(const void* in, void* out, const DSParams& p, 
     TOut* o = static_cast<TOut*>(out);
     if (discrete) {
         if constexpr (std::is_integral<TIn>::value) {
-            hipLaunchKernelGGL((downsample_discrete_kernel<TIn, TOut>), dim3(blocks), dim3(256), 0,
-                               s, i, o, p);
+            if (p.ndim == 3 && p.win[0] == 2 && p.win[1] == 2 && p.win[2] == 2 &&
+                p.out_shape[1] <= 65535) {
+                const int64_t gx = (p.out_shape[2] + 255) / 256, gy = p.out_shape[1];
+                const int64_t gz = std::max<int64_t>(1, std::min<int64_t>(
+                    {p.out_shape[0], (int64_t)65535, 262144 / std::max<int64_t>(1, gx * gy)}));
+                hipLaunchKernelGGL((downsample3_mode_kernel<TIn, TOut>),
+                                   dim3((unsigned)gx, (unsigned)gy, (unsigned)gz), dim3(256), 0, s,
+                                   i, o, p);
+            } else {
+                hipLaunchKernelGGL((downsample_discrete_kernel<TIn, TOut>), dim3(blocks),
+                                   dim3(256), 0, s, i, o, p);
+            }
             return hipGetLastError();
         } else {
             return hipErrorInvalidValue;

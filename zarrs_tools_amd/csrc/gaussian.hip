@@ -902,12 +902,7 @@ static hipError_t launch_zyx_l(const void* in, int dtype_in, float* out, const G
     // leave most of a wide tile idle
     if constexpr (L <= 7) {
         // f32 with whole-quad output rows: the entering slice staged by LDS-DMA
-        // (ZT_GAUSS_DMA=0 turns it off: A/B runs)
-        static const bool dma_off = [] {
-            const char* e = getenv("ZT_GAUSS_DMA");
-            return e && e[0] == '0';
-        }();
-        if (quad && p.on[2] >= ZYXWide::TX && dtype_in == kF32 && !dma_off &&
+        if (quad && p.on[2] >= ZYXWide::TX && dtype_in == kF32 &&
             p.on[2] % 4 == 0 && ((uintptr_t)out & 15) == 0)
             return launch_zyx_dma<L>(static_cast<const float*>(in), out, p, s);
         if (quad && p.on[2] >= ZYXWide::TX)

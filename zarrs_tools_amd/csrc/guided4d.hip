@@ -2,21 +2,18 @@
 // alike, guided_filter.rs:117-199 with get_block clamping on all four axes).
 //
 // The box mean over (t, z, y, x) is separable and linear, so the 4-D sums are t-window sums of
-// per-timepoint 3-D box sums:  box4(f)(t) = sum_{t' in W(t)} box3(f(t')). The default is three
-// kernels (K1, then g4_tab_kernel and box3_final_kernel, described above them); ZT_G4_LEGACY=1
-// keeps the original four over the halo'd block (windows clamp at the block bounds = the array
-// bounds):
-//   K1 box3_march<float -> double>:  U3(t) = 3-D window sums of v, exact f64 (f64 sums of f32
-//       values), one z-march per (timepoint, xy tile);
-//   K2 pointwise (all t of a voxel in one thread): U4 = t-window sums of U3 (exact),
-//       u = RN(RN_f32(U4) / c4), s = (v-u)^2, a = s/(s+eps), b = (1-a)u  ->  AB (float2);
-//   K3 box3_march<float2 -> float2>: S3(t) = 3-D window sums of (a, b), f64 accumulation rounded
-//       to f32 once;
-//   K4 final (output region only): S4 = t-window sums of S3 (f64), mean = RN_f32(S4) / c4,
-//       out = RN(RN(v * mean_a) + mean_b) cast to TOut (guided_filter.rs:144-163, :101-102).
-// HBM traffic about 64 B per voxel (v read twice, U3 / AB / S3 written and read once) against the
-// separable path's ~160; every division is IEEE (correctly rounded), stage 1 exact, stage 2 with
-// f64 accumulation, so the result is closer to the reference's f64-SAT means than the 3-D kernel's.
+// per-timepoint 3-D box sums:  box4(f)(t) = sum_{t' in W(t)} box3(f(t')), and stage 2 may take
+// the t-window first: box4(a, b) = box3(tbox(a, b)). Windows clamp at the block bounds (= the
+// array bounds with the 2r halo). Two stages:
+//   stage 1 -> TAB(t) = t-window sums of (a, b) for the output timepoints (f64, rounded once),
+//       with U3 = exact f64 3-D window sums of v, U4 = t-window of U3 (exact),
+//       u = RN(RN_f32(U4) / c4), s = (v-u)^2, a = s/(s+eps), b = (1-a)u (guided_filter.rs:126-142):
+//       r <= 2: one t-march (g4_tmarch_tab_kernel), U3 never in HBM;
+//       r 3-6: K1 box3_march<float -> double> writes U3, g4_tab_kernel writes TAB over it;
+//   K3f box3_final_kernel: the box3 z-march of TAB over the output box with the final stage,
+//       mean = RN_f32(S4) / c4, out = RN(RN(v * mean_a) + mean_b) cast to TOut
+//       (guided_filter.rs:144-163, :101-102).
+// Every division is IEEE (correctly rounded), stage 1 exact, stage 2 with f64 t-sums.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -51,6 +48,15 @@ __device__ __forceinline__ void put(float2& o, const dd2& a) { o = make_float2((
 template <typename TV> __device__ __forceinline__ TV zero_v();
 template <> __device__ __forceinline__ float zero_v<float>() { return 0.0f; }
 template <> __device__ __forceinline__ float2 zero_v<float2>() { return make_float2(0.0f, 0.0f); }
+
+// compile-time loop: f(integral_constant<I>) for I in [B, E)
+template <int B, int E, typename F>
+__device__ __forceinline__ void g4_static_for(F&& f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        g4_static_for<B + 1, E>(f);
+    }
+}
 
 __device__ __forceinline__ int ccount(int i, int n, int r) {
     const int lo = i - r < 0 ? 0 : i - r;
@@ -249,183 +255,6 @@ __global__ __launch_bounds__(kNT) void box3_march_kernel(const TV* __restrict__ 
     }
 }
 
-// K2: u, s, a, b for every timepoint of a voxel (guided_filter.rs:126-142) with 4-D counts.
-// One thread per (y, x) of a 4 x 64 block (3-D grid: no 64-bit index division; 64-wide rows keep
-// a chunk's 264-wide halo'd rows 83 % busy where 256-wide rows left half the lanes idle); the T
-// values of U3 are read once into registers (T <= TMAX at compile time).
-template <int TMAX>
-__global__ __launch_bounds__(256) void g4_pointwise_kernel(const double* __restrict__ U3,
-                                                           const float* __restrict__ v,
-                                                           float2* __restrict__ AB, int T,
-                                                           int ta_ab, int tb_ab, int nz, int ny,
-                                                           int nx, int r, float eps, Str3 vs) {
-    const int64_t vol = (int64_t)nz * ny * nx;
-    const int x = blockIdx.x * kPX + threadIdx.x, y = blockIdx.y * kPY + threadIdx.y;
-    if (x >= nx || y >= ny) return;
-    const int cyx = ccount(y, ny, r) * ccount(x, nx, r);
-    for (int z = blockIdx.z; z < nz; z += gridDim.z) {
-        const int64_t i = ((int64_t)z * ny + y) * nx + x;
-        const int c3 = ccount(z, nz, r) * cyx;
-        double U[TMAX];
-#pragma unroll
-        for (int t = 0; t < TMAX; ++t) U[t] = t < T ? U3[t * vol + i] : 0.0;
-#pragma unroll
-        for (int t = 0; t < TMAX; ++t) {
-            if (t >= T || t < ta_ab || t >= tb_ab) continue;  // only the (a, b) K4 reads
-            double U4 = 0.0;
-            const int ta = max(t - r, 0), tb = min(t + r, T - 1);
-#pragma unroll
-            for (int tt = 0; tt < TMAX; ++tt)
-                if (tt >= ta && tt <= tb) U4 += U[tt];
-            const float cnt = (float)(c3 * (tb - ta + 1));
-            const float u = (float)U4 / cnt;  // summed_area_table_mean: (sum as f32) / count
-            const float d = v[t * vs.t + (int64_t)z * vs.z + (int64_t)y * vs.y + x] - u;
-            const float s = d * d;  // (v - u).powf(2.0)
-            const float a = s / (s + eps);
-            const float b = (1.0f - a) * u;
-            AB[t * vol + i] = make_float2(a, b);
-        }
-    }
-}
-
-// K4: the output region [o0, o0 + on) of the block: t-window sums of S3, means, v*ma + mb.
-template <int TMAX, typename TOut>
-__global__ __launch_bounds__(256) void g4_final_kernel(const float2* __restrict__ S3,
-                                                       const float* __restrict__ v,
-                                                       TOut* __restrict__ out, NdGeom g, int r,
-                                                       Str3 vs) {
-    const int T = (int)g.shape[0], nz = (int)g.shape[1], ny = (int)g.shape[2],
-              nx = (int)g.shape[3];
-    const int64_t vol = (int64_t)nz * ny * nx;
-    const int ox = blockIdx.x * kPX + threadIdx.x, oy = blockIdx.y * kPY + threadIdx.y;
-    if (ox >= (int)g.out_shape[3] || oy >= (int)g.out_shape[2]) return;
-    const int x = ox + (int)g.out_start[3], y = oy + (int)g.out_start[2];
-    const int cyx = ccount(y, ny, r) * ccount(x, nx, r);
-    const int t0 = (int)g.out_start[0], ont = (int)g.out_shape[0];
-    const int tlo = max(t0 - r, 0), thi = min(t0 + ont + r, T);
-    for (int oz = blockIdx.z; oz < (int)g.out_shape[1]; oz += gridDim.z) {
-        const int z = oz + (int)g.out_start[1];
-        const int64_t bi = ((int64_t)z * ny + y) * nx + x;
-        const int c3 = ccount(z, nz, r) * cyx;
-        const int64_t dbase = oz * g.out_strides[1] + oy * g.out_strides[2] + ox * g.out_strides[3];
-        // only the timepoints the output windows read (a slab's outer halo timepoints feed
-        // stage 1 alone)
-        float2 S[TMAX];
-#pragma unroll
-        for (int t = 0; t < TMAX; ++t)
-            S[t] = t >= tlo && t < thi ? S3[t * vol + bi] : make_float2(0.f, 0.f);
-#pragma unroll
-        for (int ot = 0; ot < TMAX; ++ot) {
-            if (ot >= ont) continue;
-            const int t = ot + t0;
-            const int ta = max(t - r, 0), tb = min(t + r, T - 1);
-            double sa = 0.0, sb = 0.0;
-#pragma unroll
-            for (int tt = 0; tt < TMAX; ++tt)
-                if (tt >= ta && tt <= tb) {
-                    sa += (double)S[tt].x;
-                    sb += (double)S[tt].y;
-                }
-            const float cnt = (float)(c3 * (tb - ta + 1));
-            const float ma = (float)sa / cnt, mb = (float)sb / cnt;
-            const float vv = v[t * vs.t + (int64_t)z * vs.z + (int64_t)y * vs.y + x];
-            const float o = __fadd_rn(__fmul_rn(vv, ma), mb);  // v *= ma; v += mb
-            out[dbase + ot * g.out_strides[0]] = from_f32<TOut>(o);
-        }
-    }
-}
-
-// K2 / K4 for blocks of up to TMAX = 32 timepoints (config T's (t, z) block shares: 16 output
-// timepoints plus the 2r halo): the t-window sums slide along t in registers (the radius R a
-// template parameter, so the entering and leaving timepoints are compile-time register indices)
-// instead of one masked sum per output timepoint (O(T) instead of O(T^2) adds per voxel). Values
-// past T are zero, so the running window stays exact (f64 sums of f64 / f32 values).
-template <int TMAX, int R>
-__global__ __launch_bounds__(256) void g4_pointwise_slide_kernel(const double* __restrict__ U3,
-                                                                 const float* __restrict__ v,
-                                                                 float2* __restrict__ AB, int T,
-                                                                 int ta_ab, int tb_ab, int nz,
-                                                                 int ny, int nx, float eps,
-                                                                 Str3 vs) {
-    const int64_t vol = (int64_t)nz * ny * nx;
-    const int x = blockIdx.x * kPX + threadIdx.x, y = blockIdx.y * kPY + threadIdx.y;
-    if (x >= nx || y >= ny) return;
-    const int cyx = ccount(y, ny, R) * ccount(x, nx, R);
-    for (int z = blockIdx.z; z < nz; z += gridDim.z) {
-        const int64_t i = ((int64_t)z * ny + y) * nx + x;
-        const int c3 = ccount(z, nz, R) * cyx;
-        double U[TMAX];
-#pragma unroll
-        for (int t = 0; t < TMAX; ++t) U[t] = t < T ? U3[t * vol + i] : 0.0;
-        double W = 0.0;  // window of t = 0: [0, R]
-#pragma unroll
-        for (int j = 0; j <= R && j < TMAX; ++j) W += U[j];
-#pragma unroll
-        for (int t = 0; t < TMAX; ++t) {
-            if (t > 0) {
-                if (t + R < TMAX) W += U[t + R];
-                if (t - R - 1 >= 0) W -= U[t - R - 1];
-            }
-            if (t >= T || t < ta_ab || t >= tb_ab) continue;  // only the (a, b) K4 reads
-            const int ta = max(t - R, 0), tb = min(t + R, T - 1);
-            const float cnt = (float)(c3 * (tb - ta + 1));
-            const float u = (float)W / cnt;  // summed_area_table_mean: (sum as f32) / count
-            const float d = v[t * vs.t + (int64_t)z * vs.z + (int64_t)y * vs.y + x] - u;
-            const float sq = d * d;  // (v - u).powf(2.0)
-            const float a = sq / (sq + eps);
-            const float b = (1.0f - a) * u;
-            AB[t * vol + i] = make_float2(a, b);
-        }
-    }
-}
-
-template <int TMAX, int R, typename TOut>
-__global__ __launch_bounds__(256) void g4_final_slide_kernel(const float2* __restrict__ S3,
-                                                             const float* __restrict__ v,
-                                                             TOut* __restrict__ out, NdGeom g,
-                                                             Str3 vs) {
-    const int T = (int)g.shape[0], nz = (int)g.shape[1], ny = (int)g.shape[2],
-              nx = (int)g.shape[3];
-    const int64_t vol = (int64_t)nz * ny * nx;
-    const int ox = blockIdx.x * kPX + threadIdx.x, oy = blockIdx.y * kPY + threadIdx.y;
-    if (ox >= (int)g.out_shape[3] || oy >= (int)g.out_shape[2]) return;
-    const int x = ox + (int)g.out_start[3], y = oy + (int)g.out_start[2];
-    const int cyx = ccount(y, ny, R) * ccount(x, nx, R);
-    const int t0 = (int)g.out_start[0], ont = (int)g.out_shape[0];
-    const int tlo = max(t0 - R, 0), thi = min(t0 + ont + R, T);
-    for (int oz = blockIdx.z; oz < (int)g.out_shape[1]; oz += gridDim.z) {
-        const int z = oz + (int)g.out_start[1];
-        const int64_t bi = ((int64_t)z * ny + y) * nx + x;
-        const int c3 = ccount(z, nz, R) * cyx;
-        const int64_t dbase = oz * g.out_strides[1] + oy * g.out_strides[2] + ox * g.out_strides[3];
-        float2 S[TMAX];
-#pragma unroll
-        for (int t = 0; t < TMAX; ++t)
-            S[t] = t >= tlo && t < thi ? S3[t * vol + bi] : make_float2(0.f, 0.f);
-        double sa = 0.0, sb = 0.0;  // window of t = 0
-#pragma unroll
-        for (int j = 0; j <= R && j < TMAX; ++j) {
-            sa += (double)S[j].x;
-            sb += (double)S[j].y;
-        }
-#pragma unroll
-        for (int t = 0; t < TMAX; ++t) {
-            if (t > 0) {
-                if (t + R < TMAX) { sa += (double)S[t + R].x; sb += (double)S[t + R].y; }
-                if (t - R - 1 >= 0) { sa -= (double)S[t - R - 1].x; sb -= (double)S[t - R - 1].y; }
-            }
-            const int ot = t - t0;
-            if (ot < 0 || ot >= ont || t >= T) continue;
-            const int ta = max(t - R, 0), tb = min(t + R, T - 1);
-            const float cnt = (float)(c3 * (tb - ta + 1));
-            const float ma = (float)sa / cnt, mb = (float)sb / cnt;
-            const float vv = v[t * vs.t + (int64_t)z * vs.z + (int64_t)y * vs.y + x];
-            const float o = __fadd_rn(__fmul_rn(vv, ma), mb);  // v *= ma; v += mb
-            out[dbase + ot * g.out_strides[0]] = from_f32<TOut>(o);
-        }
-    }
-}
-
 // ---- three-kernel form (round 4): stage 2 as box3 of the t-window sums ------------------------
 // box4(a, b) = box3(tbox(a, b)) (the sums are separable; stage 2 is rounded to f32 anyway), so
 //   K2t: per voxel, all T timepoints in registers: U4 = t-window of U3 (exact), u, a, b, and
@@ -484,6 +313,277 @@ __global__ __launch_bounds__(256) void g4_tab_kernel(double* __restrict__ U3T,
                 TAB[(int64_t)(tt - t0) * vol + i] = make_float2((float)sa, (float)sb);
             }
         }
+    }
+}
+
+// ---- t-march stage 1 (round 5): K1 and K2t in one kernel, no U3 in HBM --------------------------
+// One workgroup owns a 16 x 16 x 8 (x, y, z) tile of the TAB region (the output box + R, clamped to
+// the block) and marches along t. Per step t it stages v(t) on the tile + 2R apron in LDS and forms
+// U3(t) = the exact f64 3-D window sums of its voxels (x, y passes through LDS, the z pass from LDS
+// into registers); each thread keeps, for its 2 voxels, a register ring of the last 2R + 1 U3 and
+// (a, b) values, so U4 = the t-window of U3 (exact), u, a, b (guided_filter.rs:126-142 with 4-D
+// counts) and TAB = the t-window sums of (a, b) (f64, rounded to f32 once) follow R and 2R steps
+// later, exactly as g4_tab_kernel forms them from U3. The t-march is unrolled by 2R + 1 so every
+// ring slot is a compile-time register. HBM: v once (+ the apron's L2 / MALL re-reads) and TAB
+// written; the f64 U3 (8 B per input voxel written and read back) never leaves the CU.
+#ifndef G4_TM_MZ
+#define G4_TM_MZ 8  // t-march tile depth (tools/timetshare.hip A/B)
+#endif
+#ifndef G4_TM_PFD
+#define G4_TM_PFD 2  // stage loads issued this many steps ahead
+#endif
+#ifndef G4_TM_VP
+#define G4_TM_VP 4  // t-march voxels per thread (along z)
+#endif
+constexpr int kMX = 16, kMY = 16, kMZ = G4_TM_MZ;  // tile (x, y, z)
+constexpr int kMVP = G4_TM_VP, kMNT = kMX * kMY * kMZ / kMVP;  // voxels per thread; threads
+
+// Buffer (SRD) accesses of the t-march: 32-bit byte offsets from a per-step base, out-of-range
+// offsets read 0 / drop the store, so the march has no branch around a memory instruction (the
+// compiler's vmcnt accounting then keeps the next step's loads in flight across the barriers).
+using g4rsrc = __amdgpu_buffer_rsrc_t;
+typedef unsigned int u32x2g4 __attribute__((ext_vector_type(2)));
+constexpr int kG4Bad = (int)0x80000000;
+__device__ __forceinline__ g4rsrc g4_rsrc(const void* base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes,
+                                             0x00020000);
+}
+__device__ __forceinline__ float g4_ld(g4rsrc r, int off) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
+// LDS-only workgroup barrier (__syncthreads would also wait for the loads in flight)
+__device__ __forceinline__ void g4_lds_barrier() {
+    __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+__device__ __forceinline__ int g4_opaque(int v) {
+    __asm__ volatile("" : "+v"(v));
+    return v;
+}
+
+// x / d for an integer count d given rcp = RN(1/d): Markstein's correction makes the quotient
+// correctly rounded (gf_fused.hpp div_by_count: the same value as IEEE division), 3 VALU ops.
+__device__ __forceinline__ float g4_div_by_count(float x, float d, float rcp) {
+    const float q = x * rcp;
+    const float r = __builtin_fmaf(-q, d, x);
+    return __builtin_fmaf(r, rcp, q);
+}
+// s / (s + eps): rcp + one Newton step + Markstein correction, within 1 ulp (gf_fused.hpp
+// fast_div, the 3-D kernel's a); 0/0 and inf/inf give NaN as IEEE division does.
+__device__ __forceinline__ float g4_fast_div(float x, float d) {
+    float y = __builtin_amdgcn_rcpf(d);
+    const float e = __builtin_fmaf(-d, y, 1.0f);
+    y = __builtin_fmaf(e, y, y);
+    const float q = x * y;
+    const float r = __builtin_fmaf(-d, q, x);
+    return __builtin_fmaf(r, y, q);
+}
+
+// Host check of the t-march's 32-bit offsets: a staged tile (2R planes of apron) and a TAB tile
+// stay within 2 GiB of their per-step bases.
+bool g4_tmarch_offsets_fit(const int64_t* vs3, int ny, int nx, int radius) {
+    const int64_t sz = kMZ + 2 * radius, sy = kMY + 2 * radius, sx = kMX + 2 * radius;
+    const int64_t v_span = ((sz - 1) * vs3[1] + (sy - 1) * vs3[2] + sx) * 4;
+    const int64_t t_span = ((int64_t)kMZ * ny * nx) * 8;
+    return v_span < ((int64_t)1 << 31) && t_span < ((int64_t)1 << 31);
+}
+
+template <int R>
+__global__ __launch_bounds__(kMNT) void g4_tmarch_tab_kernel(const float* __restrict__ v, Str3 vs,
+                                                             float2* __restrict__ TAB, int T,
+                                                             int t0, int ont, int nz, int ny,
+                                                             int nx, int zlo, int ylo, int xlo,
+                                                             int tnx, int tny, int tnz, int ntx,
+                                                             int nty, float eps) {
+    constexpr int W = 2 * R + 1, VP = kMVP;
+    constexpr int SX = kMX + 2 * R, SY = kMY + 2 * R, SZ = kMZ + 2 * R, NS = SX * SY * SZ;
+    constexpr int NPS = (NS + kMNT - 1) / kMNT;  // staged elements per thread
+    constexpr int KX = 4, KY = 4;                // x / y sliding outputs per item
+    constexpr int NXI = SZ * SY * (kMX / KX);    // x-pass items
+    constexpr int NYI = SZ * kMX * (kMY / KY);   // y-pass items
+    static_assert(kMZ % VP == 0 && kMX * kMY * (kMZ / VP) == kMNT, "voxels cover the tile");
+    constexpr int NC = W * W * W * W;  // largest 4-D window count
+    __shared__ float Vs[SZ][SY][SX];
+    __shared__ double Xs[SZ][SY][kMX];
+    __shared__ double Ys[SZ][kMY][kMX];
+    __shared__ float rcp_tab[NC + 1];  // RN(1/c) for every window count c (div_by_count)
+    for (int c = threadIdx.x; c <= NC; c += kMNT) rcp_tab[c] = c > 0 ? 1.0f / (float)c : 0.0f;
+    g4_lds_barrier();
+
+    // XCD-aware block order (xcd_block): each XCD marches a contiguous run of neighbouring tiles
+    const int64_t nb = gridDim.x;
+    const int64_t b = blockIdx.x;
+    const int64_t lid = nb % 8 == 0 ? (b % 8) * (nb / 8) + b / 8 : b;
+    const int tx = (int)(lid % ntx), ty = (int)((lid / ntx) % nty), tz = (int)(lid / ((int64_t)ntx * nty));
+    const int x0 = xlo + tx * kMX, y0 = ylo + ty * kMY, z0 = zlo + tz * kMZ;
+    const int xend = xlo + tnx, yend = ylo + tny, zend = zlo + tnz;
+
+    // staged elements: v(t) on the tile + 2R apron, staged through LDS (one coalesced load per
+    // element; reading each x-pass item's row segment straight from global memory instead, 1.6x
+    // the load instructions, measured 1.35x slower: profiles/r05_tmarch_ab.txt). Byte offsets
+    // from plane z0 - R of a timepoint, shifted up to plane 0 when that plane lies below the
+    // block (buffer bases must not precede the allocation); kG4Bad outside the block (reads 0:
+    // the zero padding of the clamped windows).
+    const int zsh = min(z0 - R, 0);
+    const int64_t vbase = (int64_t)(z0 - R - zsh) * vs.z;
+    int soff[NPS];
+#pragma unroll
+    for (int k = 0; k < NPS; ++k) {
+        const int e = threadIdx.x + k * kMNT;
+        const int ez = e / (SY * SX), ey = (e / SX) % SY, ex = e % SX;
+        const int gz = z0 - R + ez, gy = y0 - R + ey, gx = x0 - R + ex;
+        const bool in = e < NS && gz >= 0 && gz < nz && gy >= 0 && gy < ny && gx >= 0 && gx < nx;
+        soff[k] = in ? (int)(((ez + zsh) * vs.z + gy * vs.y + gx) * 4) : kG4Bad;
+    }
+    // staged values of steps t + 1 .. t + PFD (pre[0 .. PFD - 1]): the loads of a step stay in
+    // flight for PFD steps
+    constexpr int PFD = G4_TM_PFD;
+    float pre[PFD][NPS];
+    auto load_stage = [&](float (&dst)[NPS], int t) {
+        const bool ok = (unsigned)t < (unsigned)T;
+        const g4rsrc r = g4_rsrc(v + (ok ? (int64_t)t * vs.t + vbase : 0), ok ? 0x7FFFFFF0u : 0u);
+#pragma unroll
+        for (int k = 0; k < NPS; ++k) dst[k] = g4_ld(r, g4_opaque(soff[k]));
+    };
+
+    // this thread's voxels: (x, y) and VP consecutive z
+    const int lx = threadIdx.x % kMX, ly = (threadIdx.x / kMX) % kMY,
+              lz = VP * (threadIdx.x / (kMX * kMY));
+    const int gx = x0 + lx, gy = y0 + ly;
+    bool own[VP];
+    int c3[VP], toff[VP], voff[VP];  // count; TAB and v byte offsets from the tile's plane z0
+#pragma unroll
+    for (int q = 0; q < VP; ++q) {
+        const int gz = z0 + lz + q;
+        own[q] = gx < xend && gy < yend && gz < zend;
+        c3[q] = ccount(gz, nz, R) * ccount(gy, ny, R) * ccount(gx, nx, R);
+        toff[q] = own[q] ? (((lz + q) * ny + gy) * nx + gx) * 8 : kG4Bad;
+        voff[q] = own[q] ? (int)(((lz + q) * vs.z + gy * vs.y + gx) * 4) : kG4Bad;
+    }
+    const int64_t vol = (int64_t)nz * ny * nx;
+    const int tlo = t0 - R, thi = t0 + ont + R;  // (a, b) needed on [tlo, thi)
+    const int tb = max(0, t0 - 2 * R), te = min(T, t0 + ont + 2 * R);  // U3 needed on [tb, te)
+    const int nsteps = (te - tb + 2 * R + W - 1) / W * W;
+
+    double ru[W][VP];   // U3 ring: slot (t - tb) % W holds U3(t)
+    float2 rab[W][VP];  // (a, b) ring: slot (tau - tb) % W holds ab(tau)
+    double U4[VP], SA[VP], SB[VP];  // running t-windows (exact: f64 sums of exact values)
+#pragma unroll
+    for (int q = 0; q < VP; ++q) {
+        U4[q] = SA[q] = SB[q] = 0.0;
+#pragma unroll
+        for (int j = 0; j < W; ++j) {
+            ru[j][q] = 0.0;
+            rab[j][q] = make_float2(0.f, 0.f);
+        }
+    }
+#pragma unroll
+    for (int d = 0; d < PFD; ++d) load_stage(pre[d], tb + d);
+    for (int tb0 = tb; tb0 < tb + nsteps; tb0 += W) {
+        g4_static_for<0, W>([&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            const int t = tb0 + k;
+            const int tau = t - R;  // (a, b) of this step
+            const int tp = tau - R;  // TAB of this step: the t-window [tp - R, tp + R] of (a, b)
+            // v(tau) at this thread's voxels, for s = (v - u)^2 (read early, used last)
+            float vt[VP];
+            {
+                const bool ok = (unsigned)tau < (unsigned)T;
+                const g4rsrc r = g4_rsrc(v + (ok ? (int64_t)tau * vs.t + (int64_t)z0 * vs.z : 0),
+                                         ok ? 0x7FFFFFF0u : 0u);
+#pragma unroll
+                for (int q = 0; q < VP; ++q) vt[q] = g4_ld(r, g4_opaque(voff[q]));
+            }
+            double u3[VP];
+#pragma unroll
+            for (int q = 0; q < VP; ++q) u3[q] = 0.0;
+            // stage 1 of step t; past te its U3 feeds no emitted window, so the LDS passes are
+            // skipped there (a uniform branch with no global access inside)
+            float* const Vf = &Vs[0][0][0];
+#pragma unroll
+            for (int j = 0; j < NPS; ++j)
+                if (threadIdx.x + j * kMNT < NS) Vf[threadIdx.x + j * kMNT] = pre[0][j];
+#pragma unroll
+            for (int d = 0; d + 1 < PFD; ++d)
+#pragma unroll
+                for (int j = 0; j < NPS; ++j) pre[d][j] = pre[d + 1][j];
+            load_stage(pre[PFD - 1], t + PFD);
+            if (t < te) {
+            g4_lds_barrier();
+            for (int it = threadIdx.x; it < NXI; it += kMNT) {  // x-window sums (exact f64)
+                const int row = it / (kMX / KX), sx = (it % (kMX / KX)) * KX;
+                const int ez = row / SY, ey = row % SY;
+                double s = 0.0;
+#pragma unroll
+                for (int j = 0; j <= 2 * R; ++j) s += (double)Vs[ez][ey][sx + j];
+                Xs[ez][ey][sx] = s;
+#pragma unroll
+                for (int j = 1; j < KX; ++j) {
+                    s += (double)Vs[ez][ey][sx + j + 2 * R];
+                    s -= (double)Vs[ez][ey][sx + j - 1];
+                    Xs[ez][ey][sx + j] = s;
+                }
+            }
+            g4_lds_barrier();
+            for (int it = threadIdx.x; it < NYI; it += kMNT) {  // y-window sums, lanes on x
+                const int xx = it % kMX, sy = ((it / kMX) % (kMY / KY)) * KY,
+                          ez = it / (kMX * (kMY / KY));
+                double s = 0.0;
+#pragma unroll
+                for (int j = 0; j <= 2 * R; ++j) s += Xs[ez][sy + j][xx];
+                Ys[ez][sy][xx] = s;
+#pragma unroll
+                for (int j = 1; j < KY; ++j) {
+                    s += Xs[ez][sy + j + 2 * R][xx];
+                    s -= Xs[ez][sy + j - 1][xx];
+                    Ys[ez][sy + j][xx] = s;
+                }
+            }
+            g4_lds_barrier();
+            {  // z-window sums of this thread's VP voxels (exact f64)
+                double zs[VP + 2 * R];
+#pragma unroll
+                for (int j = 0; j < VP + 2 * R; ++j) zs[j] = Ys[lz + j][ly][lx];
+                double s = 0.0;
+#pragma unroll
+                for (int j = 0; j <= 2 * R; ++j) s += zs[j];
+                u3[0] = s;
+#pragma unroll
+                for (int q = 1; q < VP; ++q) {
+                    s += zs[q + 2 * R];
+                    s -= zs[q - 1];
+                    u3[q] = s;
+                }
+            }
+            }
+            // U4(tau): the t-window [t - 2R, t] of U3, the ring after U3(t) entered
+            constexpr int su = k, sab = (k - R + W) % W;
+            const bool need_ab = tau >= tlo && tau < thi && tau >= 0 && tau < T;
+            const int ct = min(tau + R, T - 1) - max(tau - R, 0) + 1;
+            const bool emit = tp >= t0 && tp < t0 + ont;
+            const g4rsrc rt = g4_rsrc(TAB + (emit ? (int64_t)(tp - t0) * vol + (int64_t)z0 * ny * nx : 0),
+                                      emit ? 0x7FFFFFF0u : 0u);
+#pragma unroll
+            for (int q = 0; q < VP; ++q) {
+                U4[q] += u3[q];
+                U4[q] -= ru[su][q];
+                ru[su][q] = u3[q];
+                const int c = c3[q] * ct;
+                // summed_area_table_mean: RN(RN_f32(U4) / c), as IEEE division
+                const float u = g4_div_by_count((float)U4[q], (float)c, rcp_tab[min(max(c, 0), NC)]);
+                const float d = vt[q] - u;
+                const float sq = d * d;  // (v - u).powf(2.0)
+                const float a = g4_fast_div(sq, sq + eps);
+                const float2 ab = need_ab ? make_float2(a, (1.0f - a) * u) : make_float2(0.f, 0.f);
+                SA[q] += (double)ab.x;
+                SB[q] += (double)ab.y;
+                SA[q] -= (double)rab[sab][q].x;
+                SB[q] -= (double)rab[sab][q].y;
+                rab[sab][q] = ab;
+                const float2 o = make_float2((float)SA[q], (float)SB[q]);
+                __builtin_amdgcn_raw_buffer_store_b64(
+                    (u32x2g4){__float_as_uint(o.x), __float_as_uint(o.y)}, rt, g4_opaque(toff[q]), 0, 0);
+            }
+        });
     }
 }
 
@@ -699,29 +799,9 @@ hipError_t launch_box3_r(int r, const TV* in, TO* out, int T, int nz, int ny, in
 // checked by the caller (K2 / K4 hold a voxel's timepoints in registers, y is grid.y)
 bool guided4d_supports(int radius) { return radius >= 1 && radius <= 6; }
 
-// ZT_G4_LEGACY=1: the four-kernel form (K2 / K3 / K4 with the AB and S3 round trips; A/B runs)
-static bool g4_legacy() {
-    static const bool on = [] {
-        const char* e = getenv("ZT_G4_LEGACY");
-        return e && e[0] == '1';
-    }();
-    return on;
-}
-
-// ZT_G4_FINAL_RING=0: box3_final_kernel re-reads the leaving slice instead of holding the z-window
-// ring in registers (A/B runs)
-static bool g4_final_ring() {
-    static const bool on = [] {
-        const char* e = getenv("ZT_G4_FINAL_RING");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
-
 int64_t guided4d_scratch_bytes(int64_t numel, bool gather) {
-    // U3 / S3 / TAB (8 B) | AB (8 B, four-kernel form only) | v (4 B, when the input is not a
-    // contiguous f32 block)
-    return numel * ((g4_legacy() ? 16 : 8) + (gather ? 4 : 0)) + 64;
+    // U3 / TAB (8 B) | v (4 B, when the input is not a contiguous f32 block)
+    return numel * (8 + (gather ? 4 : 0)) + 64;
 }
 
 hipError_t launch_guided4d(const void* in, int dtype_in, void* out, int dtype_out,
@@ -730,9 +810,10 @@ hipError_t launch_guided4d(const void* in, int dtype_in, void* out, int dtype_ou
               nx = (int)g.shape[3];
     const int64_t n = g.numel;
     if (n <= 0 || g.out_numel <= 0) return hipSuccess;
+    if (T > 32) return hipErrorInvalidValue;
     char* base = static_cast<char*>(scratch);
-    double* U3 = reinterpret_cast<double*>(base);          // later S3 (float2) in place
-    float2* AB = reinterpret_cast<float2*>(base + n * 8);
+    double* U3 = reinterpret_cast<double*>(base);  // U3, then TAB (float2) over it
+    float2* TAB = reinterpret_cast<float2*>(base);
     // f32 with unit-stride x is read in place (strided t / z / y); other element types or
     // strides are first copied to C-order f32 in scratch
     const bool in_place = dtype_in == kF32 && g.in_strides[3] == 1;
@@ -740,7 +821,7 @@ hipError_t launch_guided4d(const void* in, int dtype_in, void* out, int dtype_ou
     Str3 vs{g.in_strides[0], g.in_strides[1], g.in_strides[2]};
     hipError_t e;
     if (!in_place) {
-        float* vv = reinterpret_cast<float*>(base + n * 16);
+        float* vv = reinterpret_cast<float*>(base + n * 8);
         for (int t = 0; t < T; ++t) {
             const size_t esz = dtype_size(dtype_in);
             e = launch_cast_to_f32_3d(static_cast<const char*>(in) + esz * t * g.in_strides[0],
@@ -751,13 +832,38 @@ hipError_t launch_guided4d(const void* in, int dtype_in, void* out, int dtype_ou
         v = vv;
         vs = Str3{(int64_t)nz * ny * nx, (int64_t)ny * nx, (int64_t)nx};
     }
-    e = launch_box3_r<float, double, double>(radius, v, U3, T, nz, ny, nx, vs, s);
-    if (e != hipSuccess) return e;
-    if (ny > 65535 || g.out_shape[2] > 65535) return hipErrorInvalidValue;  // grid.y
-    if (!g4_legacy()) {
-        // three-kernel form: K2t (u, a, b and their t-window sums for the output timepoints)
-        // then the box3 march of those with the final stage in its output (K3f)
-        const int t0 = (int)g.out_start[0], ont = (int)g.out_shape[0];
+    if (ny > 65535 || g.out_shape[2] > 65535) return hipErrorInvalidValue;  // grid.y (K2t)
+    const int t0 = (int)g.out_start[0], ont = (int)g.out_shape[0];
+    const int64_t onx = g.out_shape[3], ony = g.out_shape[2], onz = g.out_shape[1];
+    // the t-march's buffer accesses use 32-bit byte offsets from per-step tile bases
+    const int64_t vs3[3] = {vs.t, vs.z, vs.y};
+    const bool tmarch_fits = g4_tmarch_offsets_fit(vs3, ny, nx, radius);
+    if (radius <= 2 && tmarch_fits) {
+        // stage 1 and the (a, b) t-window sums in one t-march (g4_tmarch_tab_kernel): TAB on the
+        // voxels box3_final_kernel reads (the output box + R, and the plane its z-window seed
+        // adds and removes again), clamped to the block
+        const int oz0 = (int)g.out_start[1], oy0 = (int)g.out_start[2], ox0 = (int)g.out_start[3];
+        const int zlo = std::max(0, oz0 - radius - 1), zhi = (int)std::min<int64_t>(nz, oz0 + onz + radius);
+        const int ylo = std::max(0, oy0 - radius), yhi = (int)std::min<int64_t>(ny, oy0 + ony + radius);
+        const int xlo = std::max(0, ox0 - radius), xhi = (int)std::min<int64_t>(nx, ox0 + onx + radius);
+        const int ntx = (xhi - xlo + kMX - 1) / kMX, nty = (yhi - ylo + kMY - 1) / kMY,
+                  ntz = (zhi - zlo + kMZ - 1) / kMZ;
+        const int64_t nb = (int64_t)ntx * nty * ntz;
+        if (nb <= 0) return hipSuccess;
+        if (nb > 0x7FFFFFFF) return hipErrorInvalidValue;
+#define ZT_G4_TM(RR)                                                                              \
+        hipLaunchKernelGGL((g4_tmarch_tab_kernel<RR>), dim3((unsigned)nb), dim3(kMNT), 0, s, v, vs, \
+                           TAB, T, t0, ont, nz, ny, nx, zlo, ylo, xlo, xhi - xlo, yhi - ylo,      \
+                           zhi - zlo, ntx, nty, eps)
+        if (radius == 1) ZT_G4_TM(1);
+        else ZT_G4_TM(2);
+#undef ZT_G4_TM
+    } else {
+        // K1: U3 = exact 3-D window sums of every timepoint; K2t: u, a, b and their t-window
+        // sums for the output timepoints, written over U3 (a thread reads every U3 of its voxel
+        // first)
+        e = launch_box3_r<float, double, double>(radius, v, U3, T, nz, ny, nx, vs, s);
+        if (e != hipSuccess) return e;
         const int64_t pgx = (nx + kPX - 1) / kPX, pgy = (ny + kPY - 1) / kPY;
         const dim3 pgrid((unsigned)pgx, (unsigned)pgy,
                          (unsigned)std::min<int64_t>(nz, std::max<int64_t>(1, 65536 / (pgy * pgx) + 1)));
@@ -780,22 +886,22 @@ hipError_t launch_guided4d(const void* in, int dtype_in, void* out, int dtype_ou
         };
         if (T <= 4) k2r(std::integral_constant<int, 4>{});
         else if (T <= 16) k2r(std::integral_constant<int, 16>{});
-        else if (T <= 32) k2r(std::integral_constant<int, 32>{});
-        else return hipErrorInvalidValue;
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-        const int64_t onx = g.out_shape[3], ony = g.out_shape[2], onz = g.out_shape[1];
-        const bool ring = g4_final_ring() && (int64_t)ny * nx < ((int64_t)1 << 31);
-        const int tiles_x = (int)((onx + kTX - 1) / kTX), tiles_y = (int)((ony + kTY - 1) / kTY);
-        const int64_t tiles = (int64_t)tiles_x * tiles_y;
-        int nseg = (int)std::max<int64_t>(
-            1, std::min<int64_t>((onz + 15) / 16, (4096 + tiles * ont - 1) / (tiles * ont)));
-        const int zseg = (int)((onz + nseg - 1) / nseg);
-        nseg = (int)((onz + zseg - 1) / zseg);
-        const int64_t gx = tiles * nseg;
-        if (gx > 0x7FFFFFFF || ont > 65535) return hipErrorInvalidValue;
-        const float2* TAB = reinterpret_cast<const float2*>(U3);
-        const dim3 fg((unsigned)gx, (unsigned)ont);
-        switch (radius) {
+        else k2r(std::integral_constant<int, 32>{});
+    }
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    // K3f: box3 z-march of TAB with the final stage (the z-window ring in registers; 32-bit plane
+    // indices, so planes past 2^31 elements take the re-reading form)
+    const bool ring = (int64_t)ny * nx < ((int64_t)1 << 31);
+    const int tiles_x = (int)((onx + kTX - 1) / kTX), tiles_y = (int)((ony + kTY - 1) / kTY);
+    const int64_t tiles = (int64_t)tiles_x * tiles_y;
+    int nseg = (int)std::max<int64_t>(
+        1, std::min<int64_t>((onz + 15) / 16, (4096 + tiles * ont - 1) / (tiles * ont)));
+    const int zseg = (int)((onz + nseg - 1) / nseg);
+    nseg = (int)((onz + zseg - 1) / zseg);
+    const int64_t gx = tiles * nseg;
+    if (gx > 0x7FFFFFFF || ont > 65535) return hipErrorInvalidValue;
+    const dim3 fg((unsigned)gx, (unsigned)ont);
+    switch (radius) {
 #define ZT_G4_K3F(RR)                                                                             \
     case RR:                                                                                      \
         if (ring)                                                                                 \
@@ -805,82 +911,11 @@ hipError_t launch_guided4d(const void* in, int dtype_in, void* out, int dtype_ou
             hipLaunchKernelGGL((box3_final_kernel<RR, false, kTY>), fg, dim3(kNT), 0, s, TAB, v,   \
                                out, dtype_out, g, zseg, tiles_x, tiles_y, vs);                    \
         break;
-            ZT_G4_K3F(1) ZT_G4_K3F(2) ZT_G4_K3F(3) ZT_G4_K3F(4) ZT_G4_K3F(5) ZT_G4_K3F(6)
+        ZT_G4_K3F(1) ZT_G4_K3F(2) ZT_G4_K3F(3) ZT_G4_K3F(4) ZT_G4_K3F(5) ZT_G4_K3F(6)
 #undef ZT_G4_K3F
-        default: return hipErrorInvalidValue;
-        }
-        return hipGetLastError();
+    default: return hipErrorInvalidValue;
     }
-    // (a, b) are needed only within R timepoints of the output's (a slab's halo timepoints
-    // beyond that feed stage 1 alone)
-    const int ta_ab = std::max<int>(0, (int)g.out_start[0] - radius);
-    const int tb_ab = std::min<int>(T, (int)(g.out_start[0] + g.out_shape[0]) + radius);
-    const int64_t pgx = (nx + kPX - 1) / kPX, pgy = (ny + kPY - 1) / kPY;
-    const dim3 pgrid((unsigned)pgx, (unsigned)pgy,
-                     (unsigned)std::min<int64_t>(nz, std::max<int64_t>(1, 65536 / (pgy * pgx) + 1)));
-    const dim3 pblock(kPX, kPY);
-    if (T <= 4)
-        hipLaunchKernelGGL(g4_pointwise_kernel<4>, pgrid, pblock, 0, s, U3, v, AB, T, ta_ab,
-                           tb_ab, nz, ny, nx, radius, eps, vs);
-    else if (T <= 16)
-        hipLaunchKernelGGL(g4_pointwise_kernel<16>, pgrid, pblock, 0, s, U3, v, AB, T, ta_ab,
-                           tb_ab, nz, ny, nx, radius, eps, vs);
-    else if (T <= 32) {  // config T's (t, z) block shares: 16 output timepoints + the 2r halo
-        switch (radius) {
-#define ZT_G4_K2(RR)                                                                              \
-    case RR:                                                                                      \
-        hipLaunchKernelGGL((g4_pointwise_slide_kernel<32, RR>), pgrid, pblock, 0, s, U3, v, AB, T, \
-                           ta_ab, tb_ab, nz, ny, nx, eps, vs);                                    \
-        break;
-        ZT_G4_K2(1) ZT_G4_K2(2) ZT_G4_K2(3) ZT_G4_K2(4) ZT_G4_K2(5) ZT_G4_K2(6)
-#undef ZT_G4_K2
-        default: return hipErrorInvalidValue;
-        }
-    } else
-        return hipErrorInvalidValue;
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    float2* S3 = reinterpret_cast<float2*>(U3);
-    {  // K3 on the timepoints whose (a, b) sums K4 reads
-        const int64_t vol = (int64_t)nz * ny * nx;
-        e = launch_box3_r<float2, dd2, float2>(radius, AB + ta_ab * vol, S3 + ta_ab * vol,
-                                               tb_ab - ta_ab, nz, ny, nx,
-                                               Str3{vol, (int64_t)ny * nx, (int64_t)nx}, s);
-    }
-    if (e != hipSuccess) return e;
-    const int64_t onx = g.out_shape[3], ony = g.out_shape[2], onz = g.out_shape[1];
-    const int64_t fgx = (onx + kPX - 1) / kPX, fgy = (ony + kPY - 1) / kPY;
-    const dim3 fgrid((unsigned)fgx, (unsigned)fgy,
-                     (unsigned)std::min<int64_t>(onz, std::max<int64_t>(1, 65536 / (fgy * fgx) + 1)));
-    e = hipErrorInvalidValue;
-    if (T <= 4) {
-        ZT_DISPATCH_DTYPE(dtype_out, TO,
-            hipLaunchKernelGGL((g4_final_kernel<4, TO>), fgrid, dim3(kPX, kPY), 0, s, S3, v,
-                               static_cast<TO*>(out), g, radius, vs);
-            e = hipGetLastError())
-    } else if (T <= 16) {
-        ZT_DISPATCH_DTYPE(dtype_out, TO,
-            hipLaunchKernelGGL((g4_final_kernel<16, TO>), fgrid, dim3(kPX, kPY), 0, s, S3, v,
-                               static_cast<TO*>(out), g, radius, vs);
-            e = hipGetLastError())
-    } else {
-        auto launch = [&](auto rr) {
-            constexpr int RR = decltype(rr)::value;
-            ZT_DISPATCH_DTYPE(dtype_out, TO,
-                hipLaunchKernelGGL((g4_final_slide_kernel<32, RR, TO>), fgrid, dim3(kPX, kPY), 0,
-                                   s, S3, v, static_cast<TO*>(out), g, vs);
-                e = hipGetLastError())
-        };
-        switch (radius) {
-        case 1: launch(std::integral_constant<int, 1>{}); break;
-        case 2: launch(std::integral_constant<int, 2>{}); break;
-        case 3: launch(std::integral_constant<int, 3>{}); break;
-        case 4: launch(std::integral_constant<int, 4>{}); break;
-        case 5: launch(std::integral_constant<int, 5>{}); break;
-        case 6: launch(std::integral_constant<int, 6>{}); break;
-        default: return hipErrorInvalidValue;
-        }
-    }
-    return e;
+    return hipGetLastError();
 }
 
 }  // namespace zt

@@ -318,13 +318,8 @@ int run_guided4d(zt_ctx* ctx, int dtype_in, const void* in, const int64_t* shape
         if (shape[d] > INT32_MAX) return fail(ZT_ERR_INVALID_PARAMETERS, "extent exceeds 2^31-1");
     }
     if (g.numel == 0 || g.out_numel == 0) return ZT_OK;
-    // T <= 4, r <= 2: the one-march kernel (g4_fused.hip); ZT_G4_FUSED=0 forces the four-kernel
-    // path (A/B runs and tests)
-    static const bool fused_off = [] {
-        const char* e = getenv("ZT_G4_FUSED");
-        return e && e[0] == '0';
-    }();
-    if (!fused_off && zt::guided4d_fused_supports(radius, g)) {
+    // T <= 4, r <= 2: the one-march kernel (g4_fused.hip)
+    if (zt::guided4d_fused_supports(radius, g)) {
         bool contiguous = dtype_in == zt::kF32;
         int64_t st = 1;
         for (int d = 3; d >= 0; --d) {
@@ -1066,11 +1061,10 @@ int zt_pyramid_downsample(zt_ctx* ctx, int dtype, const void* level0, const int6
     const void* src = level0;
     int64_t cur[ZT_MAX_DIMS];
     std::copy(shape, shape + ndim, cur);
-    // 2x2x2 mean levels fuse, up to three per launch, while every extent of a fused level's
-    // input is >= 2 (window 2 on every axis); other levels run one launch each
-    const bool fusable = ndim == 3 && !discrete && factor[0] == 2 && factor[1] == 2 &&
-                         factor[2] == 2 && zt::pyramid_fused_dtype(dtype) &&
-                         std::getenv("ZT_PYRAMID_UNFUSED") == nullptr;
+    // 2x2x2 mean or mode levels fuse, up to three per launch, while every extent of a fused
+    // level's input is >= 2 (window 2 on every axis); other levels run one launch each
+    const bool fusable = ndim == 3 && factor[0] == 2 && factor[1] == 2 && factor[2] == 2 &&
+                         zt::pyramid_fused_dtype(dtype, discrete != 0);
     auto level_shape = [&](int i) -> const int64_t* {  // shape of level i (0 = input)
         return i == 0 ? shape : shapes.data() + (size_t)(i - 1) * ndim;
     };
@@ -1094,7 +1088,8 @@ int zt_pyramid_downsample(zt_ctx* ctx, int dtype, const void* level0, const int6
                     return fail(ZT_ERR_INVALID_PARAMETERS, "null level pointer");
                 DeviceGuard g(ctx->device);
                 if (ctx->timed) ZT_HIP(hipEventRecord(ctx->ev0, ctx->cur));
-                hipError_t e = zt::launch_pyramid_fused(src, dtype, sh3, k, level_ptrs + i, ctx->cur);
+                hipError_t e = zt::launch_pyramid_fused(src, dtype, sh3, k, level_ptrs + i,
+                                                       discrete != 0, ctx->cur);
                 if (e != hipSuccess) return hip_fail(e, "fused pyramid launch");
                 if (ctx->timed) ZT_HIP(hipEventRecord(ctx->ev1, ctx->cur));
             }

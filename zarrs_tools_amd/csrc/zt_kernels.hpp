@@ -91,13 +91,14 @@ struct DSParams {
 };
 hipError_t launch_downsample(const void* in, int dtype_in, void* out, int dtype_out,
                              const DSParams& p, bool discrete, hipStream_t s);
-// nl (2 or 3) fused 2x2x2 mean pyramid levels: shapes[0] = input, shapes[1..nl] = levels
-// (each floor(previous / 2), every extent of shapes[0..nl-1] >= 2); outs[l-1] = level l.
-bool pyramid_fused_dtype(int dtype);
+// nl (2 or 3) fused 2x2x2 mean (or mode: discrete) pyramid levels: shapes[0] = input,
+// shapes[1..nl] = levels (each floor(previous / 2), every extent of shapes[0..nl-1] >= 2);
+// outs[l-1] = level l.
+bool pyramid_fused_dtype(int dtype, bool discrete);
 // the fused pyramid grid (launch_pyramid_fused) for a level-1 shape fits the launch limits
 bool pyramid_fused_grid_fits(const int64_t* level1_shape);
 hipError_t launch_pyramid_fused(const void* in, int dtype, const int64_t (*shapes)[3], int nl,
-                                void* const* outs, hipStream_t s);
+                                void* const* outs, bool discrete, hipStream_t s);
 
 // Gaussian pass along one axis (gaussian.hip): input region outer x n x inner (C order), output
 // outer x on x inner with output k reading input positions around o0 + k (replicate edges).
