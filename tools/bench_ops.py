@@ -33,39 +33,61 @@ def timed(fn, stream, reps):
     return e0.elapsed_time(e1) / reps
 
 
-def bench_pyramid(n, reps, levels):
+def bench_pyramid(n, reps, levels, discrete=False, dtype="uint16"):
     import numpy as np
     import torch
     import zarrs_tools_amd as zt
     from oracle import oracle as O
     ctx = zt.default_context(0)
     x = zt.synth_u16((n, n, n))
+    if dtype == "uint8":  # the low byte of the u16 noise: 256 values, ties and majorities
+        x = (x.view(torch.int16) & 0xFF).to(torch.uint8) if not discrete else \
+            (x.view(torch.int16) & 0x7).to(torch.uint8)
+    elif discrete:  # few distinct values, so the mode is not mostly a tie of eight
+        x = (x.view(torch.int16) & 0x7).view(torch.uint16)
+    esz = x.element_size()
     torch.cuda.synchronize()
     shapes = zt.pyramid_level_shapes((n, n, n), (2, 2, 2), levels)
-    ms = timed(lambda: zt.pyramid(x, (2, 2, 2), levels, ctx=ctx),
+    ms = timed(lambda: zt.pyramid(x, (2, 2, 2), levels, discrete=discrete, ctx=ctx),
                torch.cuda.current_stream(), reps)
+    # parity (bit-exact): a 64^3 level-0 block aligned to 2^levels, its levels from the oracle
+    lv = zt.pyramid(x, (2, 2, 2), levels, discrete=discrete, ctx=ctx)
+    blk = x[:64, 64:128, 128:192].cpu().numpy()
+    cur, exact = blk, True
+    for k, t in enumerate(lv):
+        cur = O.downsample(cur, dtype, (2, 2, 2), dtype, discrete=discrete)
+        f = 2 ** (k + 1)
+        got = t[:64 // f, 64 // f:128 // f, 128 // f:192 // f].cpu().numpy()
+        exact = exact and np.array_equal(got, cur)
+    del lv
     # compulsory bytes: level 0 read once + every level written once (fused launches never
     # read an intermediate level back); per_level: each level's input read + output written
-    prev, nbytes, per_level = (n, n, n), 2 * n ** 3, 0
+    prev, nbytes, per_level = (n, n, n), esz * n ** 3, 0
     for s in shapes:
-        per_level += 2 * (int(np.prod(prev)) + int(np.prod(s)))
-        nbytes += 2 * int(np.prod(s))
+        per_level += esz * (int(np.prod(prev)) + int(np.prod(s)))
+        nbytes += esz * int(np.prod(s))
         prev = s
     gbs = nbytes / (ms / 1e3) / 1e9
     # CPU: the oracle's level-1 downsample of a 256^3 sample (single thread)
     sample = O.synth_u16((256, 256, 256))
+    if discrete:
+        sample = (sample & 0x7).astype(np.dtype(dtype))
+    elif dtype == "uint8":
+        sample = (sample & 0xFF).astype(np.uint8)
     t0 = time.perf_counter()
-    O.downsample(sample, "uint16", (2, 2, 2), "uint16")
+    O.downsample(sample, dtype, (2, 2, 2), dtype, discrete=discrete)
     cpu_s = time.perf_counter() - t0
-    return {"op": "zarrs_ome mean pyramid (device-resident)", "config":
-            {"level0": [n] * 3, "dtype": "uint16", "factor": [2, 2, 2], "levels": len(shapes)},
+    return {"op": f"zarrs_ome {'mode (--discrete)' if discrete else 'mean'} pyramid "
+                  "(device-resident)", "config":
+            {"level0": [n] * 3, "dtype": dtype, "factor": [2, 2, 2], "levels": len(shapes)},
+            "parity_bit_exact": bool(exact),
             "ms": round(ms, 4), "input_gvox_per_s": round(n ** 3 / (ms / 1e3) / 1e9, 3),
             "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
                          "algorithmic_bytes": nbytes, "per_level_bytes": per_level},
             "cpu_baseline": {"input_gvox_per_s": round(256 ** 3 / cpu_s / 1e9, 4), "cores": 1,
-                             "kind": "port", "sample": "level 1 of a 256^3 uint16 block, "
-                             "oracle downsample (C restatement of downsample.rs:72-97)"}}
+                             "kind": "port", "sample": f"level 1 of a 256^3 {dtype} block, "
+                             "oracle downsample (C restatement of downsample.rs:72-120)"}}
 
 
 def bench_gaussian(n, reps):
@@ -210,6 +232,10 @@ def main():
             return
     if "pyramid" in only:
         print(json.dumps(bench_pyramid(a.pyramid_size, a.reps, a.levels)), flush=True)
+    if "pyramid_discrete" in only:
+        for dt in ("uint16", "uint8"):
+            print(json.dumps(bench_pyramid(a.pyramid_size, a.reps, a.levels, True, dt)),
+                  flush=True)
     if "gaussian" in only:
         print(json.dumps(bench_gaussian(a.gaussian_size, a.reps)), flush=True)
 

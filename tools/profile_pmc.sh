@@ -12,7 +12,7 @@ run() {  # name counters...
   local name=$1; shift
   [[ " $PASSES " == *" $name "* ]] || return 0
   timeout -k 10 240 rocprofv3 --pmc "$@" -d "$ROOT/$OUT/$name" -o run --output-format csv -- \
-    python3 "$ROOT/bench.py" --no-cpu-baseline "${BENCH_ARGS[@]}" > "$ROOT/$OUT/$name.log" 2>&1
+    python3 "$ROOT/bench.py" --no-cpu-baseline --no-extra "${BENCH_ARGS[@]}" > "$ROOT/$OUT/$name.log" 2>&1
   echo "$name rc=$?"
 }
 BENCH_ARGS=("$@")

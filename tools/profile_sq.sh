@@ -9,7 +9,7 @@ cd /tmp && export TMPDIR=/tmp
 run() {
   local name=$1; shift
   timeout -k 10 240 rocprofv3 --pmc "$@" -d "$ROOT/$OUT/$name" -o run --output-format csv -- \
-    python3 "$ROOT/bench.py" --no-cpu-baseline --steps 1 --warmup 0 "${BENCH_ARGS[@]}" > "$ROOT/$OUT/$name.log" 2>&1
+    python3 "$ROOT/bench.py" --no-cpu-baseline --no-extra --steps 1 --warmup 0 "${BENCH_ARGS[@]}" > "$ROOT/$OUT/$name.log" 2>&1
   echo "$name rc=$?"
 }
 BENCH_ARGS=("$@")

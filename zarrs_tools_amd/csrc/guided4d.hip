@@ -327,10 +327,10 @@ __global__ __launch_bounds__(256) void g4_tab_kernel(double* __restrict__ U3T,
 // ring slot is a compile-time register. HBM: v once (+ the apron's L2 / MALL re-reads) and TAB
 // written; the f64 U3 (8 B per input voxel written and read back) never leaves the CU.
 #ifndef G4_TM_MZ
-#define G4_TM_MZ 8  // t-march tile depth (tools/timetshare.hip A/B)
+#define G4_TM_MZ 12  // t-march tile depth (tools/timetshare.hip A/B: 12 beats 8 by 4 %)
 #endif
 #ifndef G4_TM_PFD
-#define G4_TM_PFD 2  // stage loads issued this many steps ahead
+#define G4_TM_PFD 1  // stage loads issued this many steps ahead (1-4 within 2 %)
 #endif
 #ifndef G4_TM_VP
 #define G4_TM_VP 4  // t-march voxels per thread (along z)
@@ -360,24 +360,6 @@ __device__ __forceinline__ int g4_opaque(int v) {
     return v;
 }
 
-// x / d for an integer count d given rcp = RN(1/d): Markstein's correction makes the quotient
-// correctly rounded (gf_fused.hpp div_by_count: the same value as IEEE division), 3 VALU ops.
-__device__ __forceinline__ float g4_div_by_count(float x, float d, float rcp) {
-    const float q = x * rcp;
-    const float r = __builtin_fmaf(-q, d, x);
-    return __builtin_fmaf(r, rcp, q);
-}
-// s / (s + eps): rcp + one Newton step + Markstein correction, within 1 ulp (gf_fused.hpp
-// fast_div, the 3-D kernel's a); 0/0 and inf/inf give NaN as IEEE division does.
-__device__ __forceinline__ float g4_fast_div(float x, float d) {
-    float y = __builtin_amdgcn_rcpf(d);
-    const float e = __builtin_fmaf(-d, y, 1.0f);
-    y = __builtin_fmaf(e, y, y);
-    const float q = x * y;
-    const float r = __builtin_fmaf(-d, q, x);
-    return __builtin_fmaf(r, y, q);
-}
-
 // Host check of the t-march's 32-bit offsets: a staged tile (2R planes of apron) and a TAB tile
 // stay within 2 GiB of their per-step bases.
 bool g4_tmarch_offsets_fit(const int64_t* vs3, int ny, int nx, int radius) {
@@ -401,13 +383,11 @@ __global__ __launch_bounds__(kMNT) void g4_tmarch_tab_kernel(const float* __rest
     constexpr int NXI = SZ * SY * (kMX / KX);    // x-pass items
     constexpr int NYI = SZ * kMX * (kMY / KY);   // y-pass items
     static_assert(kMZ % VP == 0 && kMX * kMY * (kMZ / VP) == kMNT, "voxels cover the tile");
-    constexpr int NC = W * W * W * W;  // largest 4-D window count
+    // (padded LDS pitches that remove the x pass's 4-way bank conflicts measured within 1 %:
+    //  profiles/r05_tmarch_ab.txt, call J; the index arithmetic costs the registers instead)
     __shared__ float Vs[SZ][SY][SX];
     __shared__ double Xs[SZ][SY][kMX];
     __shared__ double Ys[SZ][kMY][kMX];
-    __shared__ float rcp_tab[NC + 1];  // RN(1/c) for every window count c (div_by_count)
-    for (int c = threadIdx.x; c <= NC; c += kMNT) rcp_tab[c] = c > 0 ? 1.0f / (float)c : 0.0f;
-    g4_lds_barrier();
 
     // XCD-aware block order (xcd_block): each XCD marches a contiguous run of neighbouring tiles
     const int64_t nb = gridDim.x;
@@ -466,10 +446,10 @@ __global__ __launch_bounds__(kMNT) void g4_tmarch_tab_kernel(const float* __rest
 
     double ru[W][VP];   // U3 ring: slot (t - tb) % W holds U3(t)
     float2 rab[W][VP];  // (a, b) ring: slot (tau - tb) % W holds ab(tau)
-    double U4[VP], SA[VP], SB[VP];  // running t-windows (exact: f64 sums of exact values)
+    double SA[VP], SB[VP];  // running t-window sums of (a, b) (exact: f64 sums of f32 values)
 #pragma unroll
     for (int q = 0; q < VP; ++q) {
-        U4[q] = SA[q] = SB[q] = 0.0;
+        SA[q] = SB[q] = 0.0;
 #pragma unroll
         for (int j = 0; j < W; ++j) {
             ru[j][q] = 0.0;
@@ -511,16 +491,17 @@ __global__ __launch_bounds__(kMNT) void g4_tmarch_tab_kernel(const float* __rest
             g4_lds_barrier();
             for (int it = threadIdx.x; it < NXI; it += kMNT) {  // x-window sums (exact f64)
                 const int row = it / (kMX / KX), sx = (it % (kMX / KX)) * KX;
-                const int ez = row / SY, ey = row % SY;
+                const float* src = &Vs[0][0][0] + row * SX + sx;
+                double* dst = &Xs[0][0][0] + row * kMX + sx;
                 double s = 0.0;
 #pragma unroll
-                for (int j = 0; j <= 2 * R; ++j) s += (double)Vs[ez][ey][sx + j];
-                Xs[ez][ey][sx] = s;
+                for (int j = 0; j <= 2 * R; ++j) s += (double)src[j];
+                dst[0] = s;
 #pragma unroll
                 for (int j = 1; j < KX; ++j) {
-                    s += (double)Vs[ez][ey][sx + j + 2 * R];
-                    s -= (double)Vs[ez][ey][sx + j - 1];
-                    Xs[ez][ey][sx + j] = s;
+                    s += (double)src[j + 2 * R];
+                    s -= (double)src[j - 1];
+                    dst[j] = s;
                 }
             }
             g4_lds_barrier();
@@ -564,15 +545,15 @@ __global__ __launch_bounds__(kMNT) void g4_tmarch_tab_kernel(const float* __rest
                                       emit ? 0x7FFFFFF0u : 0u);
 #pragma unroll
             for (int q = 0; q < VP; ++q) {
-                U4[q] += u3[q];
-                U4[q] -= ru[su][q];
                 ru[su][q] = u3[q];
-                const int c = c3[q] * ct;
-                // summed_area_table_mean: RN(RN_f32(U4) / c), as IEEE division
-                const float u = g4_div_by_count((float)U4[q], (float)c, rcp_tab[min(max(c, 0), NC)]);
+                double U4 = 0.0;  // the ring's sum (exact: any order)
+#pragma unroll
+                for (int j = 0; j < W; ++j) U4 += ru[j][q];
+                const float cnt = (float)(c3[q] * ct);
+                const float u = (float)U4 / cnt;  // summed_area_table_mean (IEEE division)
                 const float d = vt[q] - u;
                 const float sq = d * d;  // (v - u).powf(2.0)
-                const float a = g4_fast_div(sq, sq + eps);
+                const float a = sq / (sq + eps);
                 const float2 ab = need_ab ? make_float2(a, (1.0f - a) * u) : make_float2(0.f, 0.f);
                 SA[q] += (double)ab.x;
                 SB[q] += (double)ab.y;
