@@ -43,6 +43,9 @@
 #ifndef GF_STY
 #define GF_STY 16  // XCD super-tile: tiles along y
 #endif
+#ifndef GF_P5_HOIST
+#define GF_P5_HOIST 0  // P5's LDS reads issued before P3 in C0 (A/B: tools/timek.sh)
+#endif
 #ifndef GF_WAVE_SKIP
 #define GF_WAVE_SKIP 1  // P4: idle waves branch around the phase
 #endif
@@ -852,14 +855,20 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     // every P3 segment lies inside the apron: unconditional Lab stores (a guard lets the compiler
     // sink the second pair's pointwise chain into it, serialising the pairs)
     constexpr bool kRowsWhole = C::E1Y % C::K3 == 0;
-    auto do_p3 = [&](int tid, int zc) {  // y-window (f64) of Hx -> U; a, b -> Lab
+    auto p3_load = [&](int tid, SA (&vin)[C::K3 + 2 * R]) {  // P3's Hx column segment
         const int item = tid - C::T3;
         if (item < 0) return;
         const int col = item % C::E1X, sg = item / C::E1X;
         const SA* src = Hx + (sg * C::K3) * C::PH + col;
-        SA vin[C::K3 + 2 * R], U[C::K3];
 #pragma unroll
         for (int j = 0; j < C::K3 + 2 * R; ++j) vin[j] = src[j * C::PH];
+    };
+    auto do_p3 = [&](int tid, int zc, const SA (&vin)[C::K3 + 2 * R]) {
+        // y-window (f64) of Hx -> U; a, b -> Lab
+        const int item = tid - C::T3;
+        if (item < 0) return;
+        const int col = item % C::E1X, sg = item / C::E1X;
+        SA U[C::K3];
         slide_sums_exact<R, C::K3>(vin, U);
         f2* lab = reinterpret_cast<f2*>(Lab);
         f2 Uf[NP3], vv[NP3], fc[NP3], rc[NP3], a[NP3], bb[NP3];
@@ -946,12 +955,16 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     // position P of block B+1 is suffix_B(P+1) + prefix_{B+1}(P). ~3 packed adds per output
     // instead of an f64 running sum (10 ops).
     rsrc_t ro5;  // the output slice P5 stores to this step
-    auto do_p5 = [&](int tid, int zc, auto slot_c) {  // y-window -> slice sums; z; out -> global
+    auto p5_load = [&](int tid, f2 (&vin)[K5 + 2 * R]) {  // P5's Hab column segment
         const int col5 = tid % TX, seg5 = tid / TX;
         const f2* src = reinterpret_cast<const f2*>(Hab) + (seg5 * K5) * C::PB + col5;
-        f2 vin[K5 + 2 * R], s2[K5];
 #pragma unroll
         for (int j = 0; j < K5 + 2 * R; ++j) vin[j] = src[j * C::PB];
+    };
+    auto do_p5 = [&](int tid, int zc, auto slot_c, const f2 (&vin)[K5 + 2 * R]) {
+        // y-window -> slice sums; z; out -> global
+        const int col5 = tid % TX, seg5 = tid / TX;
+        f2 s2[K5];
         core_window_sums<R, K5>(vin, s2);
         constexpr int P = decltype(slot_c)::value;
         f2 AB[K5];
@@ -1076,9 +1089,24 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
             // C0: P3(i) + P5(i-1) (LDS and registers only). P5 runs unconditionally, so no
             // branch separates its stores from the loads waited on later (the first call's slice
             // lies in no emitted window, and its stores go to a zero-record descriptor)
-            do_p3(tid, i);
-            if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(1);
-            do_p5(tid, i - 1, std::integral_constant<int, (k + W - 1) % W>{});
+            f2 vin5[K5 + 2 * R];
+            SA vin3[C::K3 + 2 * R];
+            if constexpr (GF_P5_HOIST == 2) {
+                // both phases' LDS reads first; P5's arithmetic covers P3's read latency
+                p5_load(tid, vin5);
+                p3_load(tid, vin3);
+                if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(1);
+                do_p5(tid, i - 1, std::integral_constant<int, (k + W - 1) % W>{}, vin5);
+                if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(3);
+                do_p3(tid, i, vin3);
+            } else {
+                if constexpr (GF_P5_HOIST == 1) p5_load(tid, vin5);  // in flight under P3
+                p3_load(tid, vin3);
+                do_p3(tid, i, vin3);
+                if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(1);
+                if constexpr (GF_P5_HOIST == 0) p5_load(tid, vin5);
+                do_p5(tid, i - 1, std::integral_constant<int, (k + W - 1) % W>{}, vin5);
+            }
             lds_barrier();
             if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(3);
             // C1: the loads of the next step, P12(i+1), P4(i). Every wait here is for a load
