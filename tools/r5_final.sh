@@ -1,0 +1,22 @@
+#!/bin/bash
+# Round-5 final profiling pass (GPU box, repo root), every step under its own time limit:
+#   bench.py line (headline + extra legs, cpu_baseline, parity); kernel-trace stats of it;
+#   PMC passes of the headline kernel (SQ, FETCH, WRITE, TCC) and of G2; FETCH / WRITE of the
+#   other extra legs; pmc_traffic.json keyed to this build; the bench line again with traffic.
+set -u
+OUT=gpurun_out/r5final
+ROOT=$(pwd)
+mkdir -p $OUT
+timeout -k 10 500 python3 bench.py > $OUT/bench_first.json 2> $OUT/bench_first.err || exit 1
+( cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $ROOT/$OUT/kt -o run --output-format csv -- python3 $ROOT/bench.py --no-cpu-baseline --parity-chunks 0 --steps 5 --warmup 1 > $ROOT/$OUT/kt.log 2>&1 ) || exit 1
+tools/profile_pmc.sh $OUT/pmc --steps 1 --warmup 0 --parity-chunks 0 || exit 1
+python3 tools/pmc_summary.py $OUT/pmc gf3d $((2048*2048*2048)) > $OUT/pmc_summary.txt
+PASSES="fetch write" tools/profile_pmc.sh $OUT/pmc_g2 --size 1024 --radius 2 --steps 1 --warmup 0 --parity-chunks 0 || exit 1
+rm -f profiles/pmc_traffic.json
+python3 tools/make_traffic_json.py $OUT/pmc profiles/pmc_traffic.json 2048 4 || exit 1
+python3 tools/make_traffic_json.py $OUT/pmc_g2 profiles/pmc_traffic.json 1024 2 || exit 1
+tools/profile_pmc_legs.sh $OUT/legs t_share pyramid_octant gaussian || exit 1
+python3 tools/make_traffic_json.py --legs $OUT/legs profiles/pmc_traffic.json t_share pyramid_octant gaussian || exit 1
+cp profiles/pmc_traffic.json $OUT/pmc_traffic.json
+timeout -k 10 500 python3 bench.py > $OUT/bench_final.json 2> $OUT/bench_final.err || exit 1
+echo done > $OUT/done

@@ -43,9 +43,6 @@
 #ifndef GF_STY
 #define GF_STY 16  // XCD super-tile: tiles along y
 #endif
-#ifndef GF_P5_HOIST
-#define GF_P5_HOIST 0  // P5's LDS reads issued before P3 in C0 (A/B: tools/timek.sh)
-#endif
 #ifndef GF_WAVE_SKIP
 #define GF_WAVE_SKIP 1  // P4: idle waves branch around the phase
 #endif
@@ -1089,24 +1086,15 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
             // C0: P3(i) + P5(i-1) (LDS and registers only). P5 runs unconditionally, so no
             // branch separates its stores from the loads waited on later (the first call's slice
             // lies in no emitted window, and its stores go to a zero-record descriptor)
-            f2 vin5[K5 + 2 * R];
+            // (each phase's LDS reads issued right before its arithmetic: hoisting P5's, or both
+            //  phases', ahead of P3 measured +1-4 %, profiles/r05_c0_hoist.txt)
             SA vin3[C::K3 + 2 * R];
-            if constexpr (GF_P5_HOIST == 2) {
-                // both phases' LDS reads first; P5's arithmetic covers P3's read latency
-                p5_load(tid, vin5);
-                p3_load(tid, vin3);
-                if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(1);
-                do_p5(tid, i - 1, std::integral_constant<int, (k + W - 1) % W>{}, vin5);
-                if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(3);
-                do_p3(tid, i, vin3);
-            } else {
-                if constexpr (GF_P5_HOIST == 1) p5_load(tid, vin5);  // in flight under P3
-                p3_load(tid, vin3);
-                do_p3(tid, i, vin3);
-                if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(1);
-                if constexpr (GF_P5_HOIST == 0) p5_load(tid, vin5);
-                do_p5(tid, i - 1, std::integral_constant<int, (k + W - 1) % W>{}, vin5);
-            }
+            p3_load(tid, vin3);
+            do_p3(tid, i, vin3);
+            if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(1);
+            f2 vin5[K5 + 2 * R];
+            p5_load(tid, vin5);
+            do_p5(tid, i - 1, std::integral_constant<int, (k + W - 1) % W>{}, vin5);
             lds_barrier();
             if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(3);
             // C1: the loads of the next step, P12(i+1), P4(i). Every wait here is for a load

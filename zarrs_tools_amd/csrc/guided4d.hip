@@ -590,13 +590,18 @@ __device__ __forceinline__ void store_dtype(void* out, int dtype, int64_t i, flo
 // reach into the block's halo (zero outside the block: the clamped windows). The leaving slice
 // comes from a register ring when it fits (box3_ring), as in box3_march_kernel.
 // TYF: output tile height (kTY; 64 x 32 tiles measured 55.9 against 54.0 ms on the T share)
-template <int R, bool RING, int TYF>
+// F32 (f32 output, unit x strides, 32-bit offsets checked on the host: box3_final_f32_fits):
+// every global access is a buffer access with an out-of-range offset instead of a branch, the
+// step barriers wait for LDS only and the march runs whole blocks of 2R + 1 steps (the padded
+// steps store nothing), so the next step's TAB loads stay in flight across the barriers.
+template <int R, bool RING, int TYF, bool F32 = false>
 __global__ __launch_bounds__(RING ? kTX * TYF / 2 : kNT) void box3_final_kernel(
     const float2* __restrict__ TAB,
                                                          const float* __restrict__ v,
                                                          void* __restrict__ out, int dtype_out,
                                                          NdGeom g, int zseg, int tiles_x,
                                                          int tiles_y, Str3 vs) {
+    static_assert(!F32 || RING, "the buffer-access form is the ring march");
     // RING: two outputs per thread in the y-window (512 threads for 64 x 16 tiles), so a thread
     // owns half the apron points and its ring fits without cutting occupancy
     constexpr int NT = RING ? kTX * TYF / 2 : kNT, KY = kTX * TYF / NT;
@@ -638,12 +643,41 @@ __global__ __launch_bounds__(RING ? kTX * TYF / 2 : kNT) void box3_final_kernel(
     }
     float2* const Zf = &Z[0][0];
     auto load = [&](int z, int k) -> float2 {
-        return (pidx[k] >= 0 && z >= 0 && z < nz) ? vol[(int64_t)z * plane + pidx[k]]
-                                                   : make_float2(0.f, 0.f);
+        if constexpr (F32) {
+            const bool ok = (unsigned)z < (unsigned)nz;
+            const g4rsrc r = g4_rsrc(vol + (ok ? (int64_t)z * plane : 0), ok ? 0x7FFFFFF0u : 0u);
+            const u32x2g4 q = __builtin_amdgcn_raw_buffer_load_b64(
+                r, g4_opaque(pidx[k] >= 0 ? (int)pidx[k] * 8 : kG4Bad), 0, 0);
+            return make_float2(__uint_as_float(q.x), __uint_as_float(q.y));
+        } else {
+            return (pidx[k] >= 0 && z >= 0 && z < nz) ? vol[(int64_t)z * plane + pidx[k]]
+                                                       : make_float2(0.f, 0.f);
+        }
+    };
+    auto step_barrier = [] {
+        if constexpr (F32) g4_lds_barrier();
+        else box3_barrier();
+    };
+    // F32: v of this thread's outputs of step z, loaded before the step's TAB prefetch so that
+    // waiting for it does not wait for the prefetch (vmcnt counts in issue order)
+    auto v_load = [&](int z, float (&vv)[KY]) {
+        if constexpr (F32) {
+            const int tx = threadIdx.x % kTX, sy = (threadIdx.x / kTX) * KY;
+            const int gx = x0 + tx;
+            const bool zok = z < z1;
+            const g4rsrc rv = g4_rsrc(v + (zok ? t * vs.t + (int64_t)z * vs.z : 0),
+                                      zok ? 0x7FFFFFF0u : 0u);
+#pragma unroll
+            for (int j = 0; j < KY; ++j) {
+                const int gy = y0 + sy + j;
+                const bool in = gx < ox1 && gy < oy1;
+                vv[j] = g4_ld(rv, g4_opaque(in ? (int)((gy * vs.y + gx) * 4) : kG4Bad));
+            }
+        }
     };
     // x / y windows of the Z slice of output slice z and the final stage
-    auto xy_final = [&](int z) {
-        box3_barrier();
+    auto xy_final = [&](int z, const float (&vvp)[KY]) {
+        step_barrier();
         for (int it = threadIdx.x; it < EY * (kTX / kKX); it += NT) {
             const int ey = it / (kTX / kKX), sx = (it % (kTX / kKX)) * kKX;
             float2 sacc = make_float2(0.f, 0.f);
@@ -657,10 +691,10 @@ __global__ __launch_bounds__(RING ? kTX * TYF / 2 : kNT) void box3_final_kernel(
                 X[ey][sx + j] = sacc;
             }
         }
-        box3_barrier();
+        step_barrier();
         const int tx = threadIdx.x % kTX, sy = (threadIdx.x / kTX) * KY;
         const int gx = x0 + tx;
-        const int czx = ccount(z, nz, R) * ccount(gx, nx, R) * ct;
+        const int czx = ccount(min(z, nz - 1), nz, R) * ccount(gx, nx, R) * ct;
         float2 sacc = make_float2(0.f, 0.f);
 #pragma unroll
         for (int j = 0; j <= 2 * R; ++j) acc_add(sacc, X[sy + j][tx]);
@@ -671,7 +705,22 @@ __global__ __launch_bounds__(RING ? kTX * TYF / 2 : kNT) void box3_final_kernel(
                 acc_sub(sacc, X[sy + j - 1][tx]);
             }
             const int gy = y0 + sy + j;
-            if (gx < ox1 && gy < oy1) {
+            if constexpr (F32) {
+                // z past the segment (padded steps): zero-record descriptors, nothing stored
+                const bool zok = z < z1;
+                const bool in = gx < ox1 && gy < oy1;
+                const float cnt = (float)(czx * ccount(min(gy, ny - 1), ny, R));
+                const float ma = (float)sacc.x / cnt, mb = (float)sacc.y / cnt;
+                const float o = __fadd_rn(__fmul_rn(vvp[j], ma), mb);  // v *= ma; v += mb
+                const g4rsrc ro = g4_rsrc(
+                    static_cast<float*>(out) +
+                        (zok ? ot * g.out_strides[0] + (int64_t)(z - oz0) * g.out_strides[1] : 0),
+                    zok ? 0x7FFFFFF0u : 0u);
+                __builtin_amdgcn_raw_buffer_store_b32(
+                    __float_as_uint(o), ro,
+                    g4_opaque(in ? (int)(((gy - oy0) * g.out_strides[2] + (gx - ox0)) * 4) : kG4Bad),
+                    0, 2);
+            } else if (gx < ox1 && gy < oy1) {
                 const float cnt = (float)(czx * ccount(gy, ny, R));
                 const float ma = (float)sacc.x / cnt, mb = (float)sacc.y / cnt;
                 const float vv = v[t * vs.t + (int64_t)z * vs.z + (int64_t)gy * vs.y + gx];
@@ -701,7 +750,7 @@ __global__ __launch_bounds__(RING ? kTX * TYF / 2 : kNT) void box3_final_kernel(
 #pragma unroll
             for (int j = 0; j < W; ++j) {
                 const int z = zb + j;
-                if (z < z1) {  // uniform per workgroup
+                if (F32 || z < z1) {  // uniform per workgroup (F32: padded steps store nothing)
 #pragma unroll
                     for (int k = 0; k < NPT; ++k) {
                         acc_add(zs[k], pa[k]);
@@ -709,9 +758,11 @@ __global__ __launch_bounds__(RING ? kTX * TYF / 2 : kNT) void box3_final_kernel(
                         ring[j][k] = pa[k];
                         if (zoff[k] >= 0) Zf[zoff[k]] = make_float2((float)zs[k].x, (float)zs[k].y);
                     }
+                    float vv[KY];
+                    v_load(z, vv);
 #pragma unroll
                     for (int k = 0; k < NPT; ++k) pa[k] = load(z + 1 + R, k);
-                    xy_final(z);
+                    xy_final(z, vv);
                 }
             }
         }
@@ -734,12 +785,14 @@ __global__ __launch_bounds__(RING ? kTX * TYF / 2 : kNT) void box3_final_kernel(
                 acc_sub(zs[k], ps[k]);
                 if (zoff[k] >= 0) Zf[zoff[k]] = make_float2((float)zs[k].x, (float)zs[k].y);
             }
+            float vv[KY] = {};
+            v_load(z, vv);  // F32 only (the generic form reads v in xy_final)
 #pragma unroll
             for (int k = 0; k < NPT; ++k) {
                 pa[k] = load(z + 1 + R, k);
                 ps[k] = load(z - R, k);
             }
-            xy_final(z);
+            xy_final(z, vv);
         }
     }
 }
@@ -873,6 +926,12 @@ hipError_t launch_guided4d(const void* in, int dtype_in, void* out, int dtype_ou
     // K3f: box3 z-march of TAB with the final stage (the z-window ring in registers; 32-bit plane
     // indices, so planes past 2^31 elements take the re-reading form)
     const bool ring = (int64_t)ny * nx < ((int64_t)1 << 31);
+    // f32 output with unit x strides and 32-bit byte offsets within a TAB plane, a v plane and
+    // an output plane: the buffer-access march
+    const bool f32_fast = dtype_out == kF32 && g.out_strides[3] == 1 &&
+                          (int64_t)ny * nx * 8 < ((int64_t)1 << 31) &&
+                          ((ny - 1) * vs.y + nx) * 4 < ((int64_t)1 << 31) &&
+                          ((ony - 1) * g.out_strides[2] + onx) * 4 < ((int64_t)1 << 31);
     const int tiles_x = (int)((onx + kTX - 1) / kTX), tiles_y = (int)((ony + kTY - 1) / kTY);
     const int64_t tiles = (int64_t)tiles_x * tiles_y;
     int nseg = (int)std::max<int64_t>(
@@ -885,7 +944,10 @@ hipError_t launch_guided4d(const void* in, int dtype_in, void* out, int dtype_ou
     switch (radius) {
 #define ZT_G4_K3F(RR)                                                                             \
     case RR:                                                                                      \
-        if (ring)                                                                                 \
+        if (ring && f32_fast)                                                                     \
+            hipLaunchKernelGGL((box3_final_kernel<RR, true, kTY, true>), fg, dim3(kTX * kTY / 2), 0,\
+                               s, TAB, v, out, dtype_out, g, zseg, tiles_x, tiles_y, vs);         \
+        else if (ring)                                                                            \
             hipLaunchKernelGGL((box3_final_kernel<RR, true, kTY>), fg, dim3(kTX * kTY / 2), 0, s, TAB,\
                                v, out, dtype_out, g, zseg, tiles_x, tiles_y, vs);                 \
         else                                                                                      \
