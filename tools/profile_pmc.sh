@@ -1,6 +1,6 @@
 #!/bin/bash
 # rocprofv3 counter passes for the guided-filter kernel (run on the GPU box from the repo root).
-# Usage: [PASSES="fetch write"] tools/profile_pmc.sh OUTDIR [bench args...]
+# Usage: [PASSES="fetch write lds"] tools/profile_pmc.sh OUTDIR [bench args...]
 # Each --pmc pass is its own run (kernel-trace only; no sys/runtime trace with counters).
 set -u
 OUT=$1; shift
@@ -21,3 +21,4 @@ run sq2 SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_
 run fetch FETCH_SIZE || exit 1
 run write WRITE_SIZE || exit 1
 run tcc TCC_HIT_sum TCC_MISS_sum || exit 1
+run lds SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_LDS_ADDR_CONFLICT SQ_LDS_UNALIGNED_STALL SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU || exit 1

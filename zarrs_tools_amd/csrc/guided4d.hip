@@ -332,6 +332,12 @@ __global__ __launch_bounds__(256) void g4_tab_kernel(double* __restrict__ U3T,
 #ifndef G4_TM_PFD
 #define G4_TM_PFD 1  // stage loads issued this many steps ahead (1-4 within 2 %)
 #endif
+#ifndef G4_TM_KX
+#define G4_TM_KX 4  // t-march x-pass outputs per item
+#endif
+#ifndef G4_TM_KY
+#define G4_TM_KY 4  // t-march y-pass outputs per item
+#endif
 #ifndef G4_TM_VP
 #define G4_TM_VP 4  // t-march voxels per thread (along z)
 #endif
@@ -379,7 +385,7 @@ __global__ __launch_bounds__(kMNT) void g4_tmarch_tab_kernel(const float* __rest
     constexpr int W = 2 * R + 1, VP = kMVP;
     constexpr int SX = kMX + 2 * R, SY = kMY + 2 * R, SZ = kMZ + 2 * R, NS = SX * SY * SZ;
     constexpr int NPS = (NS + kMNT - 1) / kMNT;  // staged elements per thread
-    constexpr int KX = 4, KY = 4;                // x / y sliding outputs per item
+    constexpr int KX = G4_TM_KX, KY = G4_TM_KY;  // x / y sliding outputs per item
     constexpr int NXI = SZ * SY * (kMX / KX);    // x-pass items
     constexpr int NYI = SZ * kMX * (kMY / KY);   // y-pass items
     static_assert(kMZ % VP == 0 && kMX * kMY * (kMZ / VP) == kMNT, "voxels cover the tile");
