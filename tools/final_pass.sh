@@ -1,10 +1,10 @@
 #!/bin/bash
-# Round-5 final profiling pass (GPU box, repo root), every step under its own time limit:
+# Final profiling pass of a round (GPU box, repo root), every step under its own time limit:
 #   bench.py line (headline + extra legs, cpu_baseline, parity); kernel-trace stats of it;
 #   PMC passes of the headline kernel (SQ, FETCH, WRITE, TCC) and of G2; FETCH / WRITE of the
 #   other extra legs; pmc_traffic.json keyed to this build; the bench line again with traffic.
 set -u
-OUT=gpurun_out/r5final
+OUT=gpurun_out/final
 ROOT=$(pwd)
 mkdir -p $OUT
 timeout -k 10 500 python3 bench.py > $OUT/bench_first.json 2> $OUT/bench_first.err || exit 1
