@@ -43,30 +43,6 @@
 #ifndef GF_STY
 #define GF_STY 16  // XCD super-tile: tiles along y
 #endif
-#ifndef GF_EXP_CONSTCNT
-#define GF_EXP_CONSTCNT 0  // EXPERIMENT (wrong border counts): uniform counts in every mode
-#endif
-#ifndef GF_AUX_LEAVE
-#define GF_AUX_LEAVE 0  // cache policy of the leaving-slice loads (the slice's last use)
-#endif
-#ifndef GF_AUX_P5
-#define GF_AUX_P5 0  // cache policy of P5's v loads (the slice's last use)
-#endif
-#ifndef GF_EXP_NULLV
-#define GF_EXP_NULLV 0
-#endif
-#ifndef GF_EXP_NULLS
-#define GF_EXP_NULLS 0
-#endif
-#ifndef GF_EXP_NULLA
-#define GF_EXP_NULLA 0
-#endif
-#ifndef GF_EXP_NULL_KEEP
-#define GF_EXP_NULL_KEEP 0
-#endif
-#ifndef GF_EXP_LD0
-#define GF_EXP_LD0 0
-#endif
 #ifndef GF_WAVE_SKIP
 #define GF_WAVE_SKIP 1  // P4: idle waves branch around the phase
 #endif
@@ -443,9 +419,8 @@ template <> struct Quad<uint16_t> {
         v[0] = (float)(q.x & 0xffffu); v[1] = (float)(q.x >> 16);
         v[2] = (float)(q.y & 0xffffu); v[3] = (float)(q.y >> 16);
     }
-    template <int AUX = 0>
     __device__ static void load(rsrc_t r, int off, int (&v)[4]) {
-        const u32x2 q = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, AUX);
+        const u32x2 q = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
         v[0] = (int)(q.x & 0xffffu); v[1] = (int)(q.x >> 16);
         v[2] = (int)(q.y & 0xffffu); v[3] = (int)(q.y >> 16);
     }
@@ -462,9 +437,8 @@ template <> struct Quad<uint8_t> {
         v[0] = (float)(q & 0xffu); v[1] = (float)((q >> 8) & 0xffu);
         v[2] = (float)((q >> 16) & 0xffu); v[3] = (float)(q >> 24);
     }
-    template <int AUX = 0>
     __device__ static void load(rsrc_t r, int off, int (&v)[4]) {
-        const uint32_t q = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, AUX);
+        const uint32_t q = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
         v[0] = (int)(q & 0xffu); v[1] = (int)((q >> 8) & 0xffu);
         v[2] = (int)((q >> 16) & 0xffu); v[3] = (int)(q >> 24);
     }
@@ -764,10 +738,7 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
         for (int k = 0; k < C::NQP1; ++k) {
             SI a4[4], s4[4];
             load_quad(ra, q1off[k], q1mask[k], a4);
-            if constexpr (!C::P1RING) {
-                if constexpr (EDGE) load_quad(rs, q1off[k], q1mask[k], s4);
-                else Quad<TIn>::template load<GF_AUX_LEAVE>(rs, q1off[k], s4);
-            }
+            if constexpr (!C::P1RING) load_quad(rs, q1off[k], q1mask[k], s4);
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 pa[k][e] = a4[e];
@@ -903,7 +874,7 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
             Uf[k] = (f2){(float)U[2 * k], (float)U[2 * k + 1]};
             vv[k] = (f2){vc[2 * k], vc[2 * k + 1]};  // v of slice zc, loaded a half-step ago
         }
-        if constexpr (INTERIOR || GF_EXP_CONSTCNT) {
+        if constexpr (INTERIOR) {
             // every E1 point of the tile has the full x and y windows: count = W^2 * cz(zc)
             // (wave-uniform); planes outside the domain hold no (a, b)
             const bool zin = (unsigned)zc < (unsigned)nz;
@@ -1013,7 +984,7 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
         // is clamped so its table index stays valid there
         const int zq = min(max(zo, 0), nz - 1);
         f2 rc[K5];
-        if constexpr (INTERIOR || GF_EXP_CONSTCNT) {
+        if constexpr (INTERIOR) {
             const float r = rcp_tab[W * W * clamped_count(zq, nz, R)];  // wave-uniform
 #pragma unroll
             for (int j = 0; j < K5; ++j) rc[j] = (f2){r, r};
@@ -1065,7 +1036,7 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
         for (int j = 0; j < K5; ++j) {
             const int oy = oyb + j;
             const bool ok = ox < ox_end && oy < oy_end;
-            v5[j] = Buf<TIn>::template load<GF_AUX_P5>(r, opaque(ok ? (oy * sy + ox) * ESZ : kBadOff));
+            v5[j] = Buf<TIn>::load(r, opaque(ok ? (oy * sy + ox) * ESZ : kBadOff));
         }
     };
 
@@ -1091,8 +1062,6 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     auto rs_in = [&](int64_t off, int z) {
         return make_rsrc(in_base + off, (unsigned)(z - zlo) < (unsigned)zspan ? slice_bytes : 0u);
     };
-    // EXPERIMENT (wrong output): zero-record descriptors price one stream's traffic
-    auto rs_null = [&](int64_t off, int z) { return make_rsrc(in_base + off, GF_EXP_NULL_KEEP ? slice_bytes : 0u); };
 
     // ---- pipelined march, unrolled by W so the ring slot of every P5 is a constant ----------
     // Iteration i runs
@@ -1130,25 +1099,11 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
             if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(3);
             // C1: the loads of the next step, P12(i+1), P4(i). Every wait here is for a load
             // issued a step ago.
-#if GF_EXP_NULLV
-            load_p3v(rs_null(ob + (int64_t)R * sstride, zb + R));
-            load_p5v(rs_null(ob - sstride, zb - 1));
-#else
             load_p3v(rs_in(ob + (int64_t)R * sstride, zb + R));  // P3 slice i+1
             load_p5v(rs_in(ob - sstride, zb - 1));                // P5 slice i-R
-#endif
             if constexpr (C::ORDER & 2) do_p4(tid);
             do_p12(tid, kc);
-#if GF_EXP_NULLA
-            load_p1(rs_null(ob + off_a, zb + 2 * R + 1), rs_null(ob, zb));
-#elif GF_EXP_NULLS
-            load_p1(rs_in(ob + off_a, zb + 2 * R + 1), rs_null(ob, zb));
-#elif GF_EXP_LD0
-            // EXPERIMENT (wrong output): the leaving slice re-reads the entering slice's addresses
-            load_p1(rs_in(ob + off_a, zb + 2 * R + 1), rs_in(ob + off_a, zb + 2 * R + 1));
-#else
             load_p1(rs_in(ob + off_a, zb + 2 * R + 1), r_b);
-#endif
             if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(1);
             if constexpr (!(C::ORDER & 2)) do_p4(tid);
             lds_barrier();
