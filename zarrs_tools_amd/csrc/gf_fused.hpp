@@ -43,6 +43,9 @@
 #ifndef GF_STY
 #define GF_STY 16  // XCD super-tile: tiles along y
 #endif
+#ifndef GF_P1PFD
+#define GF_P1PFD 2  // stage-1 slices prefetched this many steps ahead at r = 4 (1 or 2)
+#endif
 #ifndef GF_WAVE_SKIP
 #define GF_WAVE_SKIP 1  // P4: idle waves branch around the phase
 #endif
@@ -728,12 +731,19 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     for (int j = 0; j < K5; ++j) pre[j] = (f2){0.0f, 0.0f};
 
     // ---- phase bodies ----------------------------------------------------------------------
-    SI pa[C::NQP1][EPL], ps[C::NQP1][EPL];  // P1 inputs of the next stage-1 slice (prefetched)
+    // P1 inputs of the next PF stage-1 slices (prefetched PF steps ahead; buffer b feeds the P12
+    // of the unrolled steps k with k % PF == b)
+    // Two steps ahead at r = 4 (profiles/r05_p1_prefetch2.txt: f32 -5 % on a box where the march
+    // took 30 ms, neutral on a 28.7 ms box; u16 -1 to -3 %); one step elsewhere (r = 3 / 5 measured
+    // +0.5-0.9 %; r > 5 and the masked edge mode spill the second buffer).
+    constexpr int PF = (C::P1RING || R != 4 || EDGE) ? 1 : GF_P1PFD;
+    SI pa[PF][C::NQP1][EPL], ps[PF][C::NQP1][EPL];
     float vc[C::K3];  // v of the next P3 slice at this thread's item (prefetched)
     float v5[K5];     // v of the next P5 output slice at this thread's outputs
 #pragma unroll
     for (int j = 0; j < K5; ++j) v5[j] = 0.0f;
-    auto load_p1 = [&](rsrc_t ra, rsrc_t rs) {  // entering slice zc+R, leaving slice zc-R-1
+    auto load_p1 = [&](auto bc, rsrc_t ra, rsrc_t rs) {  // entering zc+R, leaving zc-R-1
+        constexpr int b = decltype(bc)::value;
 #pragma unroll
         for (int k = 0; k < C::NQP1; ++k) {
             SI a4[4], s4[4];
@@ -741,28 +751,29 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
             if constexpr (!C::P1RING) load_quad(rs, q1off[k], q1mask[k], s4);
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                pa[k][e] = a4[e];
-                if constexpr (!C::P1RING) ps[k][e] = s4[e];
+                pa[b][k][e] = a4[e];
+                if constexpr (!C::P1RING) ps[b][k][e] = s4[e];
             }
         }
     };
     // P12: z-window of v (f64, running) and its x-window sums on the E2 apron -> Hx. The x
     // neighbours come from the adjacent lanes' quads by DPP wave shifts (whole rows per wave),
     // so the z-window never goes through LDS.
-    auto do_p12 = [&](int tid, auto slotc) {
+    auto do_p12 = [&](int tid, auto slotc, auto bc) {
         constexpr int sl = decltype(slotc)::value;  // P1 ring slot of this step
+        constexpr int b = decltype(bc)::value;      // prefetch buffer of this step
 #pragma unroll
         for (int k = 0; k < C::NQP1; ++k) {
             int row, cq;
             const bool valid = p12_pos(tid, k, row, cq);
 #pragma unroll
             for (int e = 0; e < EPL; ++e) {
-                zv[k][e] = zv[k][e] + (SA)pa[k][e];  // entering slice (0 outside the domain)
+                zv[k][e] = zv[k][e] + (SA)pa[b][k][e];  // entering slice (0 outside the domain)
                 if constexpr (C::P1RING) {
                     zv[k][e] = zv[k][e] - (SA)ring1[sl][k][e];  // leaving slice, from the ring
-                    ring1[sl][k][e] = pa[k][e];
+                    ring1[sl][k][e] = pa[b][k][e];
                 } else {
-                    zv[k][e] = zv[k][e] - (SA)ps[k][e];  // leaving slice (0 outside the domain)
+                    zv[k][e] = zv[k][e] - (SA)ps[b][k][e];  // leaving slice (0 outside the domain)
                 }
             }
             constexpr int NB = C::NB;
@@ -1041,10 +1052,13 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     };
 
     // ---- prologue: stage 1 of the first slice up to Hx; prefetch step 1 ---------------------
-    load_p1(slice_rsrc(zc_begin + R), slice_rsrc(zc_begin - R - 1));
+    using B0 = std::integral_constant<int, 0>;
+    using BL = std::integral_constant<int, PF - 1>;
+    load_p1(BL{}, slice_rsrc(zc_begin + R), slice_rsrc(zc_begin - R - 1));
     load_p3v(slice_rsrc(zc_begin));
-    do_p12(tid0, std::integral_constant<int, W - 1>{});
-    load_p1(slice_rsrc(zc_begin + 1 + R), slice_rsrc(zc_begin - R));
+    do_p12(tid0, std::integral_constant<int, W - 1>{}, BL{});
+    load_p1(B0{}, slice_rsrc(zc_begin + 1 + R), slice_rsrc(zc_begin - R));
+    if constexpr (PF == 2) load_p1(BL{}, slice_rsrc(zc_begin + 2 + R), slice_rsrc(zc_begin + 1 - R));
     lds_barrier();
 
     // ---- slice streams: descriptors advanced by one slice per step (two 32-bit adds each)
@@ -1071,9 +1085,10 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     // from different slices. The step count is padded to a multiple of W, at least one past the
     // last stage-1 slice so that P5 / the store of the last output slice happen inside the loop:
     // no guards inside. Padded steps emit nothing (zo >= zo_end).
-    const int n_steps = (zc_end - zc_begin + 1 + W - 1) / W * W;
-    for (int i0 = zc_begin; i0 < zc_begin + n_steps; i0 += W) {
-        static_for<0, W>([&](auto kc) {
+    constexpr int UN = PF * W;  // unrolled steps: every ring slot and prefetch buffer a constant
+    const int n_steps = (zc_end - zc_begin + 1 + UN - 1) / UN * UN;
+    for (int i0 = zc_begin; i0 < zc_begin + n_steps; i0 += UN) {
+        static_for<0, UN>([&](auto kc) {
             constexpr int k = decltype(kc)::value;
             const int i = i0 + k;
             const int tid = threadIdx.x;
@@ -1102,8 +1117,12 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
             load_p3v(rs_in(ob + (int64_t)R * sstride, zb + R));  // P3 slice i+1
             load_p5v(rs_in(ob - sstride, zb - 1));                // P5 slice i-R
             if constexpr (C::ORDER & 2) do_p4(tid);
-            do_p12(tid, kc);
-            load_p1(rs_in(ob + off_a, zb + 2 * R + 1), r_b);
+            using BK = std::integral_constant<int, k % PF>;
+            do_p12(tid, std::integral_constant<int, k % W>{}, BK{});
+            if constexpr (PF == 2)  // for P12(i+3): entering slice i+3+R, leaving i+2-R
+                load_p1(BK{}, rs_in(ob + off_a + sstride, zb + 2 * R + 2), rs_in(ob + sstride, zb + 1));
+            else
+                load_p1(BK{}, rs_in(ob + off_a, zb + 2 * R + 1), r_b);
             if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(1);
             if constexpr (!(C::ORDER & 2)) do_p4(tid);
             lds_barrier();
