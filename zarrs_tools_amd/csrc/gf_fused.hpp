@@ -46,6 +46,9 @@
 #ifndef GF_P1PFD
 #define GF_P1PFD 2  // stage-1 slices prefetched this many steps ahead at r = 4 (1 or 2)
 #endif
+#ifndef GF_P1PFD_R2
+#define GF_P1PFD_R2 2  // the same at r <= 2 (stage-1 ring: entering quads only)
+#endif
 #ifndef GF_WAVE_SKIP
 #define GF_WAVE_SKIP 1  // P4: idle waves branch around the phase
 #endif
@@ -733,10 +736,11 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     // ---- phase bodies ----------------------------------------------------------------------
     // P1 inputs of the next PF stage-1 slices (prefetched PF steps ahead; buffer b feeds the P12
     // of the unrolled steps k with k % PF == b)
-    // Two steps ahead at r = 4 (profiles/r05_p1_prefetch2.txt: f32 -5 % on a box where the march
-    // took 30 ms, neutral on a 28.7 ms box; u16 -1 to -3 %); one step elsewhere (r = 3 / 5 measured
-    // +0.5-0.9 %; r > 5 and the masked edge mode spill the second buffer).
-    constexpr int PF = (C::P1RING || R != 4 || EDGE) ? 1 : GF_P1PFD;
+    // Two steps ahead at r = 4 and r <= 2 (profiles/r05_p1_prefetch2*.txt: r = 4 f32 -5 % on a
+    // box where the march took 30 ms, neutral on a 28.7 ms box, u16 -1 to -3 %; r = 1, 2 -1 to
+    // -3.6 %); one step elsewhere (r = 3 / 5 measured +0.5-0.9 %; r > 5 and the masked edge mode
+    // spill the second buffer).
+    constexpr int PF = EDGE ? 1 : R == 4 ? GF_P1PFD : R <= 2 ? GF_P1PFD_R2 : 1;
     SI pa[PF][C::NQP1][EPL], ps[PF][C::NQP1][EPL];
     float vc[C::K3];  // v of the next P3 slice at this thread's item (prefetched)
     float v5[K5];     // v of the next P5 output slice at this thread's outputs
