@@ -2,7 +2,8 @@
 # Final profiling pass of a round (GPU box, repo root), every step under its own time limit:
 #   bench.py line (headline + extra legs, cpu_baseline, parity); kernel-trace stats of it;
 #   PMC passes of the headline kernel (SQ, FETCH, WRITE, TCC) and of G2; FETCH / WRITE of the
-#   other extra legs; pmc_traffic.json keyed to this build; the bench line again with traffic.
+#   other extra legs; pmc_traffic.json keyed to this build; the bench line again with traffic;
+#   the GPU test suite and smoke().
 set -u
 OUT=gpurun_out/final
 ROOT=$(pwd)
@@ -19,4 +20,6 @@ tools/profile_pmc_legs.sh $OUT/legs t_share pyramid_octant gaussian || exit 1
 python3 tools/make_traffic_json.py --legs $OUT/legs profiles/pmc_traffic.json t_share pyramid_octant gaussian || exit 1
 cp profiles/pmc_traffic.json $OUT/pmc_traffic.json
 timeout -k 10 500 python3 bench.py > $OUT/bench_final.json 2> $OUT/bench_final.err || exit 1
+timeout -k 10 900 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread tests -m gpu > $OUT/gpu_tests.txt 2>&1 || exit 1
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $OUT/smoke.txt 2>&1 || exit 1
 echo done > $OUT/done
