@@ -94,7 +94,7 @@ class PinnedBuffer:
     hipHostMalloc flags (NON_COHERENT suits buffers only stream-ordered copies touch on the
     device side; it falls back to the default when the runtime refuses it)."""
 
-    def __init__(self, nbytes: int, flags: int = int(os.environ.get("ZT_PINNED_FLAGS", "0"), 0)):
+    def __init__(self, nbytes: int, flags: int = 0):
         self.ptr = ctypes.c_void_p()
         self.nbytes = int(nbytes)
         err = hip().hipHostMalloc(ctypes.byref(self.ptr), max(self.nbytes, 1), flags)

@@ -472,8 +472,7 @@ class OctantPool:
         # the workers never import torch (ZT_NO_TORCH=1 in the environment they are spawned with:
         # a process starts at its first submit, the warm-up, inside this setting)
         old = os.environ.get("ZT_NO_TORCH")
-        if os.environ.get("ZT_OCTANT_TORCH") != "1":  # (=1: torch workers, for A/B runs)
-            os.environ["ZT_NO_TORCH"] = "1"
+        os.environ["ZT_NO_TORCH"] = "1"
         try:
             for ex, d in zip(self.execs, self.devices):
                 ex.submit(_octant_warmup, d)
