@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define ZT_ABI_VERSION 3
+#define ZT_ABI_VERSION 4
 #define ZT_MAX_DIMS 8
 
 /* Status codes. Negative values mirror FilterError variants (src/filter/filter_error.rs:10-30). */
@@ -66,12 +66,6 @@ const char* zt_last_error(void);
 size_t zt_dtype_size(int dtype);
 /* Number of HIP devices visible (0 on a host without GPUs; never an error). */
 int zt_device_count(int* count);
-/* Fused guided-filter kernel selection (process-wide, no reference analogue): 0 = the default
- * gf3d_fused_kernel, the only variant built (the measured-slower designs of rounds 2-3 were
- * deleted; DESIGN.md §3.1 keeps their numbers); any other value is rejected. Returns the
- * previous value. */
-int zt_set_fused_variant(int variant);
-
 /* One context per (host thread, device): owns a HIP stream, events and reusable scratch. */
 int zt_ctx_create(int device, zt_ctx** out);
 int zt_ctx_destroy(zt_ctx* ctx);

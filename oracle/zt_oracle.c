@@ -540,8 +540,31 @@ int oracle_downsample_continuous(const void* in, int dtype_in, const int64_t* in
     return 0;
 }
 
-/* downsample.rs:99-120: mode of each complete window. Deterministic tie rule: smallest value
- * (the reference picks whichever HashMap entry iterates first, which is unspecified). */
+/* downsample.rs:99-120: mode of each complete window, counted over exact `TIn` keys (the
+ * reference's HashMap<TIn, usize>): the raw integer, never an f64 image of it, so distinct 64-bit
+ * values past 2^53 stay distinct. Deterministic tie rule: the smallest value in TIn's order (the
+ * reference picks whichever HashMap entry iterates first, which is unspecified). */
+static int dt_signed(int dt) {
+    return dt == OR_INT8 || dt == OR_INT16 || dt == OR_INT32 || dt == OR_INT64;
+}
+/* the element as a 64-bit key: signed types sign-extended (compare as int64), unsigned and bool
+ * zero-extended (compare as uint64) */
+static uint64_t load_key(const void* src, int dt, int64_t i) {
+    switch (dt) {
+    case OR_BOOL: case OR_UINT8: return ((const uint8_t*)src)[i];
+    case OR_INT8: return (uint64_t)(int64_t)((const int8_t*)src)[i];
+    case OR_INT16: return (uint64_t)(int64_t)((const int16_t*)src)[i];
+    case OR_INT32: return (uint64_t)(int64_t)((const int32_t*)src)[i];
+    case OR_INT64: return (uint64_t)((const int64_t*)src)[i];
+    case OR_UINT16: return ((const uint16_t*)src)[i];
+    case OR_UINT32: return ((const uint32_t*)src)[i];
+    case OR_UINT64: return ((const uint64_t*)src)[i];
+    }
+    return 0;
+}
+static int key_less(uint64_t a, uint64_t b, int sgn) {
+    return sgn ? (int64_t)a < (int64_t)b : a < b;
+}
 int oracle_downsample_discrete(const void* in, int dtype_in, const int64_t* in_shape, int ndim,
                                const int64_t* stride, void* out, int dtype_out) {
     if (dtype_in >= OR_BFLOAT16) return -2;
@@ -549,40 +572,50 @@ int oracle_downsample_discrete(const void* in, int dtype_in, const int64_t* in_s
     if (ds_shapes(in_shape, ndim, stride, win, out_shape)) return -1;
     int64_t nout = numel(out_shape, ndim), nwin = numel(win, ndim);
     int64_t oidx[OR_MAXDIM], widx[OR_MAXDIM];
-    double* vals = (double*)malloc(sizeof(double) * (nwin > 0 ? nwin : 1));
+    const int sgn = dt_signed(dtype_in);
+    uint64_t* keys = (uint64_t*)malloc(sizeof(uint64_t) * (nwin > 0 ? nwin : 1));
     for (int64_t o = 0; o < nout; ++o) {
         unravel(o, out_shape, ndim, oidx);
         for (int64_t w = 0; w < nwin; ++w) {
             unravel(w, win, ndim, widx);
             int64_t off = 0;
             for (int j = 0; j < ndim; ++j) off = off * in_shape[j] + (oidx[j] * win[j] + widx[j]);
-            vals[w] = load_as_f64(in, dtype_in, off);  /* integer types: exact for |v| < 2^53 */
+            keys[w] = load_key(in, dtype_in, off);
         }
-        double best = 0.0;
+        uint64_t best = 0;
         int64_t best_count = -1;
         for (int64_t a = 0; a < nwin; ++a) {
             int64_t count = 0;
-            for (int64_t b = 0; b < nwin; ++b) count += vals[b] == vals[a];
-            if (count > best_count || (count == best_count && vals[a] < best)) {
+            for (int64_t b = 0; b < nwin; ++b) count += keys[b] == keys[a];
+            if (count > best_count || (count == best_count && key_less(keys[a], best, sgn))) {
                 best_count = count;
-                best = vals[a];
+                best = keys[a];
             }
         }
-        /* `TIn as TOut` for integer TIn: through f64 is exact for |v| < 2^53; integer-to-integer
-         * `as` wraps in Rust, so route integers through the wrapping path. */
+        /* `TIn as TOut` (downsample.rs:117): integer -> integer wraps (two's complement bits);
+         * integer -> f32 / f64 rounds to nearest in one step; f16 / bf16 through f64 (exact below
+         * 2^53, and f16 is infinite beyond it either way). */
         switch (dtype_out) {
-        case OR_BOOL: case OR_UINT8: ((uint8_t*)out)[o] = (uint8_t)(int64_t)best; break;
-        case OR_INT8: ((int8_t*)out)[o] = (int8_t)(int64_t)best; break;
-        case OR_INT16: ((int16_t*)out)[o] = (int16_t)(int64_t)best; break;
-        case OR_INT32: ((int32_t*)out)[o] = (int32_t)(int64_t)best; break;
+        case OR_BOOL: case OR_UINT8: ((uint8_t*)out)[o] = (uint8_t)best; break;
+        case OR_INT8: ((int8_t*)out)[o] = (int8_t)best; break;
+        case OR_INT16: ((int16_t*)out)[o] = (int16_t)best; break;
+        case OR_INT32: ((int32_t*)out)[o] = (int32_t)best; break;
         case OR_INT64: ((int64_t*)out)[o] = (int64_t)best; break;
-        case OR_UINT16: ((uint16_t*)out)[o] = (uint16_t)(int64_t)best; break;
-        case OR_UINT32: ((uint32_t*)out)[o] = (uint32_t)(int64_t)best; break;
-        case OR_UINT64: ((uint64_t*)out)[o] = (uint64_t)best; break;
-        default: cast_one_from_f64(best, dtype_out, out, o); break;
+        case OR_UINT16: ((uint16_t*)out)[o] = (uint16_t)best; break;
+        case OR_UINT32: ((uint32_t*)out)[o] = (uint32_t)best; break;
+        case OR_UINT64: ((uint64_t*)out)[o] = best; break;
+        case OR_FLOAT32:
+            ((float*)out)[o] = sgn ? (float)(int64_t)best : (float)best;
+            break;
+        case OR_FLOAT64:
+            ((double*)out)[o] = sgn ? (double)(int64_t)best : (double)best;
+            break;
+        default:
+            cast_one_from_f64(sgn ? (double)(int64_t)best : (double)best, dtype_out, out, o);
+            break;
         }
     }
-    free(vals);
+    free(keys);
     return 0;
 }
 

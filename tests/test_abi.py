@@ -17,7 +17,7 @@ def test_library_exports_every_header_symbol():
 
 
 def test_abi_version():
-    assert _abi.lib().zt_abi_version() == 3
+    assert _abi.lib().zt_abi_version() == 4
 
 
 def test_device_count_never_errors():

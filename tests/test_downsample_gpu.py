@@ -53,6 +53,25 @@ def test_discrete_mode(din):
     assert np.array_equal(out, ref)
 
 
+@pytest.mark.parametrize("din,dout", [("int64", "int64"), ("uint64", "uint64"),
+                                      ("int64", "float32"), ("uint64", "float64"),
+                                      ("int64", "int32")])
+def test_discrete_mode_64bit_beyond_2pow53(din, dout):
+    """downsample.rs:113-117 counts exact TIn keys: 64-bit values past 2^53 that share one f64
+    image stay distinct, the winner is returned exactly (or rounded once by `as` for float
+    outputs, wrapped for narrower integers). Per-level kernel (2x2x2) and the N-d kernel (3x1x2)."""
+    rng = np.random.default_rng(11)
+    base = np.array([2 ** 62, 2 ** 62 + 1, 2 ** 62 + 3, 2 ** 62 + 2 ** 11, 2 ** 53 + 1],
+                    dtype=np.uint64)
+    if din == "int64":
+        base = np.concatenate([base.astype(np.int64), -base.astype(np.int64)[:3]])
+    v = base[rng.integers(0, len(base), (8, 10, 12))].astype(din)
+    for stride in [(2, 2, 2), (3, 1, 2)]:
+        ref = O.downsample(v, din, stride, dout, discrete=True)
+        out = gpu_ds(v, din, stride, dout, discrete=True)
+        np.testing.assert_array_equal(out, ref)
+
+
 def test_discrete_rejects_float():
     import torch
     with pytest.raises(zt.UnsupportedDataType):
@@ -145,10 +164,8 @@ def test_fused_mode_pyramid_equals_oracle_levels(shape, dtype, levels):
         v = rng.integers(0, 2, shape).astype(bool)
     else:
         info = np.iinfo(dtype)
-        # (the oracle compares window values as f64: 64-bit values within 2^52 stay exact)
-        lo, hi = (max(info.min, -2 ** 52), min(info.max, 2 ** 52)) if info.bits == 64 \
-            else (info.min, info.max)
-        pool = rng.integers(lo, hi, 5, dtype=dtype, endpoint=True)
+        # the full range: the oracle counts exact integer keys (64-bit values past 2^53 included)
+        pool = rng.integers(info.min, info.max, 5, dtype=dtype, endpoint=True)
         v = pool[rng.integers(0, 5, shape)]
     x = to_dev(v, dtype)
     got_levels = zt.pyramid(x, (2, 2, 2), max_levels=levels, discrete=True)

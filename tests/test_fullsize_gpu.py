@@ -9,8 +9,9 @@ compared bit-exactly with the oracle's downsample of the same input region (down
   G2  guided_filter r=2, 1024^3 f32, 256^3 chunks        (BASELINE configs[1])
   G3  guided_filter r=4, 2048^3 f32, 256^3 chunks        (configs[2], the metric)
   P   5-level 2x mean pyramid of a 2048^3 u16 per-GPU octant of configs[3]'s 4096^3
-  T   one GPU's share of configs[4]: output timepoints [8, 12) of (32, 1024^3) f32 from its
-      (12, 1024^3) input block (the 2r t-halo), chunks (4, 256^3), r=2
+  T   one GPU's share of configs[4]: rank 5's (t, z) block of the (2, 4) split of (32, 1024^3)
+      f32 (output t [16, 32) x z [256, 512) from its 20 x 264-plane halo'd input block,
+      shard.block_assignment), chunks (4, 256^3), r=2
   2-D 32768 x 16384 f32 (planes of 2 GiB: routed off the 32-bit fused path)
 """
 import numpy as np

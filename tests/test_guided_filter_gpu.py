@@ -306,8 +306,9 @@ def test_guided4d_per_chunk_and_small_eps(r):
     ((12, 8, 9, 30), (4, 4, 9, 15), 1),      # TMAX = 16
 ])
 def test_guided4d_long_series_small_eps(shape, chunk, r):
-    """The three-kernel 4-D path for blocks of 5-32 timepoints (sliding t-windows, stage 2 as box3
-    of the t-window sums with the final stage in the box3 march): whole box and per chunk equal
+    """The 4-D path for blocks of 5-32 timepoints: stage 1 as the t-march (r <= 2) or K1 +
+    g4_tab (r 3-6) writing the t-window sums of (a, b), then box3_final (their box3 with the final
+    stage in the march): whole box and per chunk equal
     the oracle at eps = 0.5 (exact stage 1)."""
     rng = np.random.default_rng(sum(shape) + r)
     v = (rng.random(shape, dtype=np.float32) * 300).astype(np.float32)
@@ -346,6 +347,46 @@ def test_guided4d_block_output_box_vs_oracle():
         got = zt.GuidedFilter(0.5, r).apply_ndarray(x, sub).cpu().numpy()
         want = ref[tuple(slice(o, o + n) for o, n in zip(a.out_start, a.out_shape))]
         assert rel_err(got, want) <= FLOAT_TOL, rank
+
+
+@pytest.mark.parametrize("r", [1, 2])
+def test_guided4d_tmarch_output_box_after_nan_scratch(r):
+    """The t-march (g4_tmarch_tab_kernel, r <= 2, T > 4) writes TAB only on the output box + r,
+    while box3_final reads whole tiles: the context scratch is first filled with NaN (a NaN
+    input's U3 / TAB), then an interior output box of a clean block must still equal the oracle
+    (stale scratch must never reach a stored output)."""
+    import torch
+    shape, chunk = (10, 24, 20, 72), (5, 8, 10, 24)
+    poison = torch.full(shape, float("nan"), dtype=torch.float32, device="cuda")
+    zt.GuidedFilter(0.5, r).apply_ndarray(poison)  # the default context: its scratch persists
+    torch.cuda.synchronize()
+    rng = np.random.default_rng(40 + r)
+    v = (rng.random(shape, dtype=np.float32) * 300).astype(np.float32)
+    ref = O.guided_filter_apply(v, chunk, 0.5, r, nthreads=8)
+    sub = zt.ArraySubset((3, 5, 4, 9), (4, 11, 9, 50))  # interior in every axis
+    got = zt.GuidedFilter(0.5, r).apply_ndarray(torch.from_numpy(v).cuda(), sub)
+    torch.cuda.synchronize()
+    want = ref[tuple(slice(s, s + n) for s, n in zip(sub.start, sub.shape))]
+    got = got.cpu().numpy()
+    assert np.isfinite(got).all()
+    assert rel_err(got, want) <= FLOAT_TOL
+
+
+@pytest.mark.parametrize("r", [1, 2])
+def test_guided4d_tmarch_strided_view(r):
+    """An in-place strided f32 view (row stride > nx, plane stride > ny * row stride) through the
+    t-march and the buffer-access box3_final: the offsets built from the global (y, x) and the
+    plane stride against the oracle of the same values made contiguous."""
+    import torch
+    rng = np.random.default_rng(60 + r)
+    big = (rng.random((9, 14, 23, 77), dtype=np.float32) * 300).astype(np.float32)
+    x = torch.from_numpy(big).cuda()[:, :, 1:-1, 2:-2]
+    assert not x.is_contiguous() and x.stride()[2] > x.shape[3]
+    v = np.ascontiguousarray(big[:, :, 1:-1, 2:-2])
+    chunk = (3, 7, 7, 25)
+    ref = O.guided_filter_apply(v, chunk, 0.5, r, nthreads=8)
+    got = zt.GuidedFilter(0.5, r).apply_ndarray(x).cpu().numpy()
+    assert rel_err(got, ref) <= FLOAT_TOL
 
 
 # ---- 4-D one-march kernel (g4_fused.hip): T <= 4 timepoints per block, r <= 2 ---------------

@@ -132,6 +132,30 @@ def test_downsample_mode_tie_smallest():
     assert O.downsample(v, "uint8", (2, 2), "uint8", discrete=True)[0, 0] == 1
 
 
+@pytest.mark.parametrize("dtype", ["int64", "uint64"])
+def test_downsample_mode_64bit_keys_exact(dtype):
+    """downsample.rs:113-117 counts exact `TIn` keys (HashMap<TIn, usize>): two 64-bit values
+    that are equal as f64 must stay distinct keys, and the winner comes back unrounded."""
+    a = 2 ** 62 + 1            # a, b: one f64 (2^62), distinct integers
+    b = 2 ** 62 + 3
+    c = 2 ** 62 + 2 ** 11      # the next f64 above 2^62
+    assert float(a) == float(b)
+    # three b, one a: b wins (as f64 keys all four would tie and come back as 2^62)
+    v = np.array([[a, b], [b, b]], dtype=dtype)
+    out = O.downsample(v, dtype, (2, 2), dtype, discrete=True)
+    assert int(out[0, 0]) == b
+    # two a, two b: a tie between distinct keys goes to the smaller value
+    v = np.array([[b, a], [a, b]], dtype=dtype)
+    assert int(O.downsample(v, dtype, (2, 2), dtype, discrete=True)[0, 0]) == a
+    # integer -> f32 rounds once (`as`): c is exactly representable
+    v = np.array([[c, c], [a, b]], dtype=dtype)
+    assert O.downsample(v, dtype, (2, 2), "float32", discrete=True)[0, 0] == np.float32(c)
+    # signed order for the tie: -1 < 1 (as uint64 bits -1 would be the larger)
+    if dtype == "int64":
+        v = np.array([[1, -1], [-1, 1]], dtype=dtype)
+        assert int(O.downsample(v, dtype, (2, 2), dtype, discrete=True)[0, 0]) == -1
+
+
 def test_synthetic_generator_definition():
     v = O.synth_step_noise_f32((2, 3, 8))
     h = O.lib().oracle_splitmix64(O.SEED ^ 5)

@@ -126,7 +126,6 @@ def lib() -> ctypes.CDLL:
         "zt_last_error": ([], ctypes.c_char_p),
         "zt_dtype_size": ([c_int], ctypes.c_size_t),
         "zt_device_count": ([ctypes.POINTER(c_int)], c_int),
-        "zt_set_fused_variant": ([c_int], c_int),
         "zt_ctx_create": ([c_int, ctypes.POINTER(vp)], c_int),
         "zt_ctx_destroy": ([vp], c_int),
         "zt_ctx_set_stream": ([vp, vp], c_int),

@@ -74,6 +74,17 @@ __global__ __launch_bounds__(256) void downsample3_kernel(const TIn* __restrict_
     }
 }
 
+// `TIn as TOut` for an integer TIn (downsample.rs:117): integer -> integer wraps; integer -> f32 /
+// f64 rounds to nearest in one step (a 64-bit value past 2^53 must not be rounded to f64 first);
+// f16 / bf16 through f64 (exact below 2^53; beyond it f16 is infinite either way).
+template <typename TOut, typename TIn>
+__device__ __forceinline__ TOut int_as(TIn v) {
+    if constexpr (std::is_integral<TOut>::value) return (TOut)v;
+    else if constexpr (std::is_same<TOut, float>::value || std::is_same<TOut, double>::value)
+        return (TOut)v;
+    else return from_f64<TOut>((double)v);
+}
+
 template <typename TIn, typename TOut>
 __global__ __launch_bounds__(256) void downsample_discrete_kernel(const TIn* __restrict__ in,
                                                                   TOut* __restrict__ out,
@@ -108,10 +119,7 @@ __global__ __launch_bounds__(256) void downsample_discrete_kernel(const TIn* __r
                 best = va;
             }
         }
-        // `TIn as TOut` for an integer TIn (downsample.rs:117): integer->integer wraps,
-        // integer->float rounds to nearest.
-        if constexpr (std::is_integral<TOut>::value) out[o] = (TOut)best;
-        else out[o] = from_f64<TOut>((double)best);
+        out[o] = int_as<TOut>(best);
     }
 }
 
@@ -343,8 +351,7 @@ __global__ __launch_bounds__(256) void downsample3_mode_kernel(const TIn* __rest
         const TIn t[8] = {src[0], src[1], src[inx], src[inx + 1], src[iny * inx],
                           src[iny * inx + 1], src[(iny + 1) * inx], src[(iny + 1) * inx + 1]};
         const TIn best = pyr_mode8<TIn>(t);
-        if constexpr (std::is_integral<TOut>::value) out[(z * ony + y) * onx + x] = (TOut)best;
-        else out[(z * ony + y) * onx + x] = from_f64<TOut>((double)best);
+        out[(z * ony + y) * onx + x] = int_as<TOut>(best);
     }
 }
 

@@ -366,11 +366,14 @@ __device__ __forceinline__ int g4_opaque(int v) {
     return v;
 }
 
-// Host check of the t-march's 32-bit offsets: a staged tile (2R planes of apron) and a TAB tile
-// stay within 2 GiB of their per-step bases.
+// Host check of the t-march's 32-bit offsets. The staged offsets (soff) and the v offsets (voff)
+// are built from the GLOBAL (y, x) of an element, relative to a per-step z-plane base, so they
+// span up to SZ - 1 (= kMZ + 2R - 1) planes of z stride plus a whole plane's (ny - 1) rows of y
+// stride plus nx elements, not one tile's; TAB offsets span kMZ planes of ny * nx pairs. Any span
+// of 2 GiB or more would wrap the (int) offset, and the buffer access would then read 0 silently.
 bool g4_tmarch_offsets_fit(const int64_t* vs3, int ny, int nx, int radius) {
-    const int64_t sz = kMZ + 2 * radius, sy = kMY + 2 * radius, sx = kMX + 2 * radius;
-    const int64_t v_span = ((sz - 1) * vs3[1] + (sy - 1) * vs3[2] + sx) * 4;
+    const int64_t sz = kMZ + 2 * radius;
+    const int64_t v_span = ((sz - 1) * vs3[1] + (int64_t)(ny - 1) * vs3[2] + nx) * 4;
     const int64_t t_span = ((int64_t)kMZ * ny * nx) * 8;
     return v_span < ((int64_t)1 << 31) && t_span < ((int64_t)1 << 31);
 }
@@ -872,7 +875,6 @@ hipError_t launch_guided4d(const void* in, int dtype_in, void* out, int dtype_ou
         v = vv;
         vs = Str3{(int64_t)nz * ny * nx, (int64_t)ny * nx, (int64_t)nx};
     }
-    if (ny > 65535 || g.out_shape[2] > 65535) return hipErrorInvalidValue;  // grid.y (K2t)
     const int t0 = (int)g.out_start[0], ont = (int)g.out_shape[0];
     const int64_t onx = g.out_shape[3], ony = g.out_shape[2], onz = g.out_shape[1];
     // the t-march's buffer accesses use 32-bit byte offsets from per-step tile bases
@@ -902,6 +904,7 @@ hipError_t launch_guided4d(const void* in, int dtype_in, void* out, int dtype_ou
         // K1: U3 = exact 3-D window sums of every timepoint; K2t: u, a, b and their t-window
         // sums for the output timepoints, written over U3 (a thread reads every U3 of its voxel
         // first)
+        if (ny > 65535 || g.out_shape[2] > 65535) return hipErrorInvalidValue;  // K1 / K2t grids
         e = launch_box3_r<float, double, double>(radius, v, U3, T, nz, ny, nx, vs, s);
         if (e != hipSuccess) return e;
         const int64_t pgx = (nx + kPX - 1) / kPX, pgy = (ny + kPY - 1) / kPY;

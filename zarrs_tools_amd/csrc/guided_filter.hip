@@ -38,10 +38,6 @@ namespace zt {
 
 bool fused_supports_radius(int radius) { return radius >= 0 && radius <= kFusedMaxRadius; }
 
-std::atomic<int>& fused_variant() {
-    static std::atomic<int> v{0};
-    return v;
-}
 int fused_tile_y(int radius) { return radius <= 4 ? 32 : 16; }  // must match gf_fused_r<R>.hip
 bool fused_direct_pair(int dtype_in, int dtype_out) {
     return fused_fast_dtype(dtype_in) && fused_fast_dtype(dtype_out);

@@ -373,11 +373,6 @@ const char* zt_last_error(void) { return g_last_error.c_str(); }
 
 size_t zt_dtype_size(int dtype) { return zt::dtype_size(dtype); }
 
-int zt_set_fused_variant(int variant) {
-    if (variant != 0) return fail(ZT_ERR_INVALID_PARAMETERS, "fused variant must be 0");
-    return zt::fused_variant().exchange(variant);
-}
-
 int zt_device_count(int* count) {
     if (!count) return fail(ZT_ERR_INVALID_PARAMETERS, "null count");
     int n = 0;

@@ -47,8 +47,6 @@ struct NdGeom {
 };
 
 bool fused_supports_radius(int radius);
-// process-wide fused-kernel selection (zt_set_fused_variant): only 0, the default, is built
-std::atomic<int>& fused_variant();
 int fused_tile_y(int radius);  // output tile height of the fused kernel for this radius
 // element-type pairs with a direct fused instantiation; others are staged through f32
 bool fused_direct_pair(int dtype_in, int dtype_out);
