@@ -63,6 +63,12 @@ def parse():
                          "config-T share, the config-P octant pyramid, the Gaussian)")
     ap.add_argument("--extra", default="g2,t_share,pyramid_octant,gaussian",
                     help="comma list of the extra legs to run")
+    ap.add_argument("--dist-extra", default="t_series,p_pyramid",
+                    help="with N > 1 ranks: the configs timed across the ranks after the headline "
+                         "(configs[4]'s (t, z) blocks, configs[3]'s octant pyramid)")
+    ap.add_argument("--dist-small", action="store_true",
+                    help="the distributed legs on (32, 512^3) / 2048^3 instead of the BASELINE "
+                         "sizes: rehearsing N ranks on one GPU (ZT_BENCH_ONE_DEVICE=1) only")
     ap.add_argument("--only-extra", default=None, metavar="LEG",
                     help="run only this extra leg, one untimed-warmup-free call (PMC passes: "
                          "tools/profile_pmc_legs.sh)")
@@ -424,6 +430,176 @@ EXTRA_LEGS = {"g2": leg_g2, "t_share": leg_t_share, "pyramid_octant": leg_pyrami
               "gaussian": leg_gaussian}
 
 
+def _dist_time(fn, dist, dev, one_dev, warmup: int, reps: int) -> float:
+    """ms per rep of `fn` on this rank, between barriers, max over ranks."""
+    import torch
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    ms = (time.perf_counter() - t0) * 1e3 / reps
+    tt = torch.tensor([ms], dtype=torch.float64, device="cpu" if one_dev else dev)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    return float(tt[0])
+
+
+def _dist_prepare(prepare, step, dist, dev, one_dev, warmup: int):
+    """Allocate a distributed leg's inputs and run its untimed warm-up calls on every rank, then
+    agree: an error on any rank (e.g. out of memory) makes every rank skip the leg together, so
+    no rank is left waiting at a barrier the others never reach. Returns the error or None."""
+    import torch
+    err = None
+    try:
+        prepare()
+        for _ in range(max(1, warmup)):
+            step()
+        torch.cuda.synchronize(dev)
+    except Exception as e:
+        err = f"{type(e).__name__}: {e}"
+    if _dist_reduce([0.0 if err else 1.0], dist.ReduceOp.MIN, dist, dev, one_dev)[0] < 1.0:
+        return err or "failed on another rank"
+    return None
+
+
+def _dist_reduce(vals, op, dist, dev, one_dev):
+    import torch
+    tt = torch.tensor(vals, dtype=torch.float64, device="cpu" if one_dev else dev)
+    dist.all_reduce(tt, op=op)
+    return [float(v) for v in tt]
+
+
+def dist_t_series(ctx, rank, world, dist, dev, one_dev, warmup, reps, small=False):
+    """configs[4] across the ranks: the (32, 1024^3) f32 series in (4, 256^3) chunks, r=2, split
+    into the 8 (t, z) blocks of shard.block_split (2 t-groups x 4 z-groups); rank g runs blocks
+    g, g + N, ... (one each at N = 8), each one GuidedFilter::apply_ndarray on its halo'd box
+    (guided_filter.rs:240-319 per block of chunks). Time = max over ranks; every rank checks a
+    (4, 32^3) output box of its first block against the oracle."""
+    import numpy as np
+    import zarrs_tools_amd as zt
+    from zarrs_tools_amd import shard
+    from zarrs_tools_amd.filter import ArraySubset
+    from oracle import oracle as O
+    gshape, chunk, nblk, radius = (32, 1024, 1024, 1024), (4, 256, 256, 256), 8, 2
+    if small:  # --dist-small: the N-rank code path rehearsed on one GPU (never the reported size)
+        gshape = (32, 512, 512, 512)
+    groups = shard.block_split(nblk, gshape, chunk, 2 * radius)
+    mine = [shard.block_assignment(b, nblk, gshape, chunk, 2 * radius, groups)
+            for b in range(rank, nblk, world)]
+    import torch
+    subs = [ArraySubset(tuple(o - i for o, i in zip(a.out_start, a.in_start)), a.out_shape)
+            for a in mine]
+    g = zt.GuidedFilter(EPS, radius)
+    res = {}
+
+    def step():
+        for x, sub in zip(res["x"], subs):
+            res["y"] = None  # the caching allocator hands the same block back
+            res["y"] = g.apply_ndarray(x, sub, ctx=ctx)
+    err = _dist_prepare(lambda: res.update(x=[zt.synth_box(a.in_start, a.in_shape, gshape,
+                                                           kind="float32", ctx=ctx)
+                                              for a in mine]), step, dist, dev, one_dev, warmup)
+    if err:
+        res.clear()
+        ctx.release_scratch()
+        torch.cuda.empty_cache()
+        return {"error": err}
+    ms = _dist_time(step, dist, dev, one_dev, 0, reps)
+    worst = float("inf")
+    try:  # parity of the first block (recomputed after timing), local to the rank
+        a = mine[0]
+        y = g.apply_ndarray(res["x"][0], subs[0], ctx=ctx)
+        box = (4, 32, 32, 32)
+        s0 = tuple(o + s // 2 for o, s in zip(a.out_start, a.out_shape))
+        coord = tuple(st // b for st, b in zip(s0, box))
+        worst = 0.0
+        for (o0, osh, ref) in O.guided_filter_synth_chunks(gshape, box, [coord], EPS, radius, 1):
+            sl = tuple(slice(p - q, p - q + s) for p, q, s in zip(o0, a.out_start, osh))
+            worst = max(worst, _max_rel(y[sl].cpu().numpy(), ref))
+        del y
+    except Exception:
+        worst = float("inf")
+    res.clear()
+    ctx.release_scratch()
+    torch.cuda.empty_cache()
+    worst = _dist_reduce([worst], dist.ReduceOp.MAX, dist, dev, one_dev)[0]
+    n = int(np.prod(gshape))
+    return {"config": "BASELINE configs[4]: (32, 1024^3) f32 series, (4, 256^3) chunks, r=2, "
+                      "its 8 (t, z) blocks over the ranks", "global_shape": list(gshape),
+            "groups_t_z": list(groups),
+            "blocks_per_rank": -(-nblk // world), "ms": round(ms, 4),
+            "value": round(n * 4 / 2 ** 30 / (ms / 1e3), 3), "unit": "GiB/s",
+            "scaling": "strong",
+            "roofline_aggregate": _roof(n * ALGO_BYTES_PER_VOXEL, ms, None),
+            "parity": {"max_rel_all_ranks": float(f"{worst:.3e}"), "tol": FLOAT_TOL,
+                       "ok": worst <= FLOAT_TOL, "box_shape": list(box)}}
+
+
+def dist_p_pyramid(ctx, rank, world, dist, dev, one_dev, warmup, reps, small=False):
+    """configs[3] across the ranks: the 4096^3 u16 volume, factor 2, 5 levels, split into its 8
+    level-0 octants (shard.octant_assignment, 2048^3 each: zarrs_ome --gpus 8); rank g runs
+    octants g, g + N, ... (the level-fused device pyramid). Time = max over ranks; every rank
+    checks its first octant's 5 levels bit-exactly on a 64^3 level-0 block."""
+    import numpy as np
+    import torch
+    import zarrs_tools_amd as zt
+    from zarrs_tools_amd import shard
+    from oracle import oracle as O
+    gshape, nblk, levels = (4096,) * 3, 8, 5
+    if small:  # --dist-small (one-GPU rehearsal)
+        gshape = (2048,) * 3
+    mine = [shard.octant_assignment(b, nblk, gshape, (2, 2, 2), levels)
+            for b in range(rank, nblk, world)]
+    res = {}
+
+    def step():
+        for j, x in enumerate(res["x"]):
+            res[j] = None
+            res[j] = zt.pyramid(x, (2, 2, 2), levels, ctx=ctx)
+    err = _dist_prepare(lambda: res.update(x=[zt.synth_box(a.start, a.shape, gshape,
+                                                           kind="uint16", ctx=ctx)
+                                              for a in mine]), step, dist, dev, one_dev, warmup)
+    if err:
+        res.clear()
+        torch.cuda.empty_cache()
+        return {"error": err}
+    ms = _dist_time(step, dist, dev, one_dev, 0, reps)
+    lv = res[0]
+    nbytes = 2 * int(np.prod(gshape)) + nblk * sum(2 * int(np.prod(t.shape)) for t in lv)
+    ok = False
+    try:  # bit-exact levels of a 64^3 block of the first octant, local to the rank
+        a = mine[0]
+        st = tuple(s + n // 2 for s, n in zip(a.start, a.shape))  # 2^5-aligned
+        cur = O.synth_block_nd(st, (64,) * 3, gshape, "uint16")
+        ok = True
+        for k, t in enumerate(lv):
+            cur = O.downsample(cur, "uint16", (2, 2, 2), "uint16")
+            f = 2 ** (k + 1)
+            sl = tuple(slice((p - q) // f, (p - q) // f + c)
+                       for p, q, c in zip(st, a.start, cur.shape))
+            ok = ok and np.array_equal(t[sl].cpu().numpy(), cur)
+    except Exception:
+        ok = False
+    del lv
+    res.clear()
+    torch.cuda.empty_cache()
+    ok = _dist_reduce([1.0 if ok else 0.0], dist.ReduceOp.MIN, dist, dev, one_dev)[0] == 1.0
+    return {"config": "BASELINE configs[3]: 4096^3 u16, factor 2, 5 levels (zarrs_ome device "
+                      "pyramid), its 8 level-0 octants over the ranks", "global_shape": list(gshape),
+            "octants_per_rank": -(-nblk // world), "ms": round(ms, 4),
+            "input_gvox_per_s": round(int(np.prod(gshape)) / (ms / 1e3) / 1e9, 3),
+            "scaling": "strong", "roofline_aggregate": _roof(nbytes, ms, None),
+            "parity": {"bit_exact_all_ranks": bool(ok), "block_shape": [64] * 3,
+                       "levels": levels}}
+
+
+DIST_LEGS = {"t_series": dist_t_series, "p_pyramid": dist_p_pyramid}
+
+
 def main():
     args = parse()
     maybe_launch(args)
@@ -589,6 +765,17 @@ def main():
             except Exception as e:  # reported, never fatal to the headline line
                 extra[name] = {"error": f"{type(e).__name__}: {e}"}
         res["extra_configs"] = extra
+    if use_dist and world > 1 and share is None and not args.no_extra and headline:
+        # configs[3] and [4] across the ranks (their own 8-way splits, round-robin over N ranks)
+        del slab, out
+        torch.cuda.empty_cache()
+        dextra = {}
+        for name in [n for n in args.dist_extra.split(",") if n]:
+            t0 = time.perf_counter()
+            dextra[name] = DIST_LEGS[name](ctx, rank, world, dist, dev, one_dev, 1, 3,
+                                           small=args.dist_small)
+            dextra[name]["wall_s"] = round(time.perf_counter() - t0, 2)
+        res["dist_configs"] = dextra
     if rank == 0:
         print(json.dumps(res), flush=True)
     ctx.close()

@@ -232,6 +232,9 @@ def main():
             return
     if "pyramid" in only:
         print(json.dumps(bench_pyramid(a.pyramid_size, a.reps, a.levels)), flush=True)
+    if "pyramid_u8" in only:  # the u8 mean pyramid (16-byte rows per lane: 2 level-3 columns)
+        print(json.dumps(bench_pyramid(a.pyramid_size, a.reps, a.levels, False, "uint8")),
+              flush=True)
     if "pyramid_discrete" in only:
         for dt in ("uint16", "uint8"):
             print(json.dumps(bench_pyramid(a.pyramid_size, a.reps, a.levels, True, dt)),

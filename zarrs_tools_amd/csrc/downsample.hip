@@ -208,15 +208,24 @@ __device__ __forceinline__ T pyr_reduce8(const T (&v)[8]) {
     else return pyr_mean8<T>(v);
 }
 
+// XPL level-3 columns per lane: a lane's level-0 rows are 8 XPL elements. 2 for u8 would load
+// 16-byte rows (one KiB per wave-instruction, as u16 rows are), but hipcc then keeps every byte of
+// the 16 rows in a VGPR of its own: 256 VGPRs, one wave per SIMD, and the 2048^3 u8 pyramids took
+// 5.66 ms (mean) / 7.86 ms (mode) against 2.76 ms for the mode at XPL 1 (round 6, tools/bench_ops.py);
+// so 1 everywhere.
+template <typename T>
+constexpr int kPyrXpl = 1;
+
 template <typename T, int NL, bool VEC, bool MODE = false>
 __global__ __launch_bounds__(256) void pyramid3_fused_kernel(const T* __restrict__ in,
                                                              T* __restrict__ l1,
                                                              T* __restrict__ l2,
                                                              T* __restrict__ l3, PyrParams p) {
-    __shared__ T lds2[4][64][2];
+    constexpr int X = kPyrXpl<T>;  // level-3 columns per lane
+    __shared__ T lds2[4][64][2 * X];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int dz = w >> 1, dy = w & 1;
-    const int64_t x3 = (int64_t)blockIdx.x * 64 + lane;
+    const int64_t x3 = ((int64_t)blockIdx.x * 64 + lane) * X;  // first level-3 column
     const int64_t by = blockIdx.y;
     const int64_t n0y = p.s[0][1], n0x = p.s[0][2];
     const int64_t n1z = p.s[1][0], n1y = p.s[1][1], n1x = p.s[1][2];
@@ -225,10 +234,10 @@ __global__ __launch_bounds__(256) void pyramid3_fused_kernel(const T* __restrict
     for (int64_t bz = blockIdx.z; bz < nz1blocks; bz += gridDim.z) {
         // level-0 block rows: z0 = 8 bz + 4 dz + a, y0 = 8 by + 4 dy + b, x0 = 8 x3 + c; all 16
         // rows are loaded before any is used (16 loads in flight per lane), kept packed
-        typedef T V8 __attribute__((ext_vector_type(8)));
+        typedef T V8 __attribute__((ext_vector_type(8 * X)));
         V8 v[4][4];
         const int64_t z0b = 8 * bz + 4 * dz, y0b = 8 * by + 4 * dy, x0b = 8 * x3;
-        const bool xfull = x0b + 8 <= n0x;
+        const bool xfull = x0b + 8 * X <= n0x;
 #pragma unroll
         for (int a = 0; a < 4; ++a)
 #pragma unroll
@@ -240,17 +249,17 @@ __global__ __launch_bounds__(256) void pyramid3_fused_kernel(const T* __restrict
                     v[a][b] = *reinterpret_cast<const V8*>(row);
                 } else {
 #pragma unroll
-                    for (int c = 0; c < 8; ++c) v[a][b][c] = (rok && x0b + c < n0x) ? row[c] : T(0);
+                    for (int c = 0; c < 8 * X; ++c) v[a][b][c] = (rok && x0b + c < n0x) ? row[c] : T(0);
                 }
             }
-        // level 1: the 2 x 2 x 4 block z1 = 4 bz + 2 dz + i, y1 = 4 by + 2 dy + j, x1 = 4 x3 + k
-        T u1[2][2][4];
+        // level 1: the 2 x 2 x 4X block z1 = 4 bz + 2 dz + i, y1 = 4 by + 2 dy + j, x1 = 4 x3 + k
+        T u1[2][2][4 * X];
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
             for (int j = 0; j < 2; ++j)
 #pragma unroll
-                for (int k = 0; k < 4; ++k) {
+                for (int k = 0; k < 4 * X; ++k) {
                     const T t[8] = {v[2 * i][2 * j][2 * k],     v[2 * i][2 * j][2 * k + 1],
                                     v[2 * i][2 * j + 1][2 * k], v[2 * i][2 * j + 1][2 * k + 1],
                                     v[2 * i + 1][2 * j][2 * k], v[2 * i + 1][2 * j][2 * k + 1],
@@ -267,21 +276,23 @@ __global__ __launch_bounds__(256) void pyramid3_fused_kernel(const T* __restrict
                 if (z1 >= n1z || y1 >= n1y) continue;  // wave-uniform
                 T* o = l1 + (z1 * n1y + y1) * n1x + x1b;
                 if constexpr (VEC) {
-                    typedef T V4 __attribute__((ext_vector_type(4)));
-                    if (x1b + 4 <= n1x) {
-                        const V4 q = {u1[i][j][0], u1[i][j][1], u1[i][j][2], u1[i][j][3]};
+                    typedef T V4 __attribute__((ext_vector_type(4 * X)));
+                    if (x1b + 4 * X <= n1x) {
+                        V4 q;
+#pragma unroll
+                        for (int k = 0; k < 4 * X; ++k) q[k] = u1[i][j][k];
                         *reinterpret_cast<V4*>(o) = q;
                         continue;
                     }
                 }
 #pragma unroll
-                for (int k = 0; k < 4; ++k)
+                for (int k = 0; k < 4 * X; ++k)
                     if (x1b + k < n1x) o[k] = u1[i][j][k];
             }
         // level 2: z2 = 2 bz + dz, y2 = 2 by + dy, x2 = 2 x3 + m
-        T u2[2];
+        T u2[2 * X];
 #pragma unroll
-        for (int m = 0; m < 2; ++m) {
+        for (int m = 0; m < 2 * X; ++m) {
             const T t[8] = {u1[0][0][2 * m], u1[0][0][2 * m + 1], u1[0][1][2 * m],
                             u1[0][1][2 * m + 1], u1[1][0][2 * m], u1[1][0][2 * m + 1],
                             u1[1][1][2 * m], u1[1][1][2 * m + 1]};
@@ -290,20 +301,25 @@ __global__ __launch_bounds__(256) void pyramid3_fused_kernel(const T* __restrict
         const int64_t z2 = 2 * bz + dz, y2 = 2 * by + dy, x2 = 2 * x3;
         if (z2 < n2z && y2 < n2y) {
             T* o = l2 + (z2 * n2y + y2) * n2x + x2;
-            if (x2 < n2x) o[0] = u2[0];
-            if (x2 + 1 < n2x) o[1] = u2[1];
+#pragma unroll
+            for (int m = 0; m < 2 * X; ++m)
+                if (x2 + m < n2x) o[m] = u2[m];
         }
         if constexpr (NL == 3) {
-            lds2[w][lane][0] = u2[0];
-            lds2[w][lane][1] = u2[1];
+#pragma unroll
+            for (int m = 0; m < 2 * X; ++m) lds2[w][lane][m] = u2[m];
             __syncthreads();
             if (w == 0) {
-                const T t[8] = {lds2[0][lane][0], lds2[0][lane][1], lds2[1][lane][0],
-                                lds2[1][lane][1], lds2[2][lane][0], lds2[2][lane][1],
-                                lds2[3][lane][0], lds2[3][lane][1]};
-                const T u3 = pyr_reduce8<T, MODE>(t);
-                if (bz < p.s[3][0] && by < p.s[3][1] && x3 < p.s[3][2])
-                    l3[(bz * p.s[3][1] + by) * p.s[3][2] + x3] = u3;
+#pragma unroll
+                for (int q = 0; q < X; ++q) {
+                    const T t[8] = {lds2[0][lane][2 * q], lds2[0][lane][2 * q + 1],
+                                    lds2[1][lane][2 * q], lds2[1][lane][2 * q + 1],
+                                    lds2[2][lane][2 * q], lds2[2][lane][2 * q + 1],
+                                    lds2[3][lane][2 * q], lds2[3][lane][2 * q + 1]};
+                    const T u3 = pyr_reduce8<T, MODE>(t);
+                    if (bz < p.s[3][0] && by < p.s[3][1] && x3 + q < p.s[3][2])
+                        l3[(bz * p.s[3][1] + by) * p.s[3][2] + x3 + q] = u3;
+                }
             }
             __syncthreads();
         }
@@ -313,13 +329,14 @@ __global__ __launch_bounds__(256) void pyramid3_fused_kernel(const T* __restrict
 template <typename T, bool MODE>
 static hipError_t launch_pyr_fused_t(const void* in, void* const* outs, const PyrParams& p,
                                      int nl, hipStream_t s) {
-    const int64_t gx = (p.s[1][2] + 255) / 256, gy = (p.s[1][1] + 3) / 4;
+    constexpr int X = kPyrXpl<T>;
+    const int64_t gx = (p.s[1][2] + 256 * X - 1) / (256 * X), gy = (p.s[1][1] + 3) / 4;
     // z capped at 128 workgroup layers, each workgroup looping over level-1 z blocks: 4096^3 u16
     // levels 1-3 in 29.2 ms against 31.8 ms for one layer per z block (tools/timepyr.hip)
     const int64_t gz = std::min<int64_t>((p.s[1][0] + 3) / 4, 128);
     if (gx > 0x7FFFFFFF || gy > 65535) return hipErrorInvalidValue;  // pyramid_fused_grid_fits
-    const bool vec = p.s[0][2] % 8 == 0 && (uintptr_t)in % (8 * sizeof(T)) == 0 &&
-                     (uintptr_t)outs[0] % (4 * sizeof(T)) == 0;
+    const bool vec = p.s[0][2] % (8 * X) == 0 && (uintptr_t)in % (8 * X * sizeof(T)) == 0 &&
+                     (uintptr_t)outs[0] % (4 * X * sizeof(T)) == 0 && p.s[1][2] % (4 * X) == 0;
     const dim3 grid((unsigned)gx, (unsigned)gy, (unsigned)gz);
     const T* i = static_cast<const T*>(in);
     T* o1 = static_cast<T*>(outs[0]);

@@ -49,6 +49,9 @@
 #ifndef GF_P1PFD_R2
 #define GF_P1PFD_R2 2  // the same at r <= 2 (stage-1 ring: entering quads only)
 #endif
+#ifndef GF_STAGGER
+#define GF_STAGGER 0  // C0 phase order P5, P3 on waves 8-15 (P3, P5 on waves 0-7)
+#endif
 #ifndef GF_WAVE_SKIP
 #define GF_WAVE_SKIP 1  // P4: idle waves branch around the phase
 #endif
@@ -1107,13 +1110,25 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
             // lies in no emitted window, and its stores go to a zero-record descriptor)
             // (each phase's LDS reads issued right before its arithmetic: hoisting P5's, or both
             //  phases', ahead of P3 measured +1-4 %, profiles/r05_c0_hoist.txt)
-            SA vin3[C::K3 + 2 * R];
-            p3_load(tid, vin3);
-            do_p3(tid, i, vin3);
-            if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(1);
-            f2 vin5[K5 + 2 * R];
-            p5_load(tid, vin5);
-            do_p5(tid, i - 1, std::integral_constant<int, (k + W - 1) % W>{}, vin5);
+            if (GF_STAGGER && __builtin_amdgcn_readfirstlane(tid >> 6) >= 8) {
+                // stagger (MI355X_MICROARCH.md "Two waves per SIMD", item 9): waves 8-15 run C0
+                // as P5 then P3, so each SIMD pairs the LDS-read head of one phase with the VALU
+                // body of the other (P3(i) and P5(i-1) are independent)
+                f2 vin5[K5 + 2 * R];
+                p5_load(tid, vin5);
+                do_p5(tid, i - 1, std::integral_constant<int, (k + W - 1) % W>{}, vin5);
+                SA vin3[C::K3 + 2 * R];
+                p3_load(tid, vin3);
+                do_p3(tid, i, vin3);
+            } else {
+                SA vin3[C::K3 + 2 * R];
+                p3_load(tid, vin3);
+                do_p3(tid, i, vin3);
+                if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(1);
+                f2 vin5[K5 + 2 * R];
+                p5_load(tid, vin5);
+                do_p5(tid, i - 1, std::integral_constant<int, (k + W - 1) % W>{}, vin5);
+            }
             lds_barrier();
             if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(3);
             // C1: the loads of the next step, P12(i+1), P4(i). Every wait here is for a load
@@ -1243,9 +1258,9 @@ inline bool fused_fast_dtype(int d) { return d == kF32 || d == kU16 || d == kU8 
         auto pick_out = [&](auto tin) -> hipError_t {                                             \
             using TI = decltype(tin);                                                             \
             switch (dout) {                                                                       \
-            case kF32: return launch_fused_auto<R, TY, NT, TI, float>(p, s);                      \
-            case kU16: return launch_fused_auto<R, TY, NT, TI, uint16_t>(p, s);                   \
-            case kU8: case kBool: return launch_fused_auto<R, TY, NT, TI, uint8_t>(p, s);         \
+            case kF32: return launch_fused_pick<R, TY, NT, TI, float>(p, s);                      \
+            case kU16: return launch_fused_pick<R, TY, NT, TI, uint16_t>(p, s);                   \
+            case kU8: case kBool: return launch_fused_pick<R, TY, NT, TI, uint8_t>(p, s);         \
             default: return hipErrorInvalidValue;                                                 \
             }                                                                                     \
         };                                                                                        \
