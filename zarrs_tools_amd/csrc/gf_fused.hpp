@@ -49,6 +49,9 @@
 #ifndef GF_P1PFD_R2
 #define GF_P1PFD_R2 2  // the same at r <= 2 (stage-1 ring: entering quads only)
 #endif
+#ifndef GF_ONEBAR
+#define GF_ONEBAR 0  // double-buffered Hx / Lab / Hab, one barrier per z-step (see the march)
+#endif
 #ifndef GF_STAGGER
 #define GF_STAGGER 0  // C0 phase order P5, P3 on waves 8-15 (P3, P5 on waves 0-7)
 #endif
@@ -547,9 +550,10 @@ struct GFConfig {
     static constexpr int SZ_LAB = al((E1Y + 1) * PA * 8);
     static constexpr int SZ_HAB = al((E1Y + 1) * PB * 8);
     static constexpr int SZ_RCP = al((W3 + 1) * 4);  // RN(1/c) for window counts c <= W^3
-    static constexpr int OFF_HX = 0, OFF_LAB = OFF_HX + SZ_HX;
-    static constexpr int OFF_HAB = OFF_LAB + SZ_LAB;
-    static constexpr int OFF_RCP = OFF_HAB + SZ_HAB;
+    static constexpr int NBUF = GF_ONEBAR ? 2 : 1;  // copies of each hand-off buffer
+    static constexpr int OFF_HX = 0, OFF_LAB = OFF_HX + NBUF * SZ_HX;
+    static constexpr int OFF_HAB = OFF_LAB + NBUF * SZ_LAB;
+    static constexpr int OFF_RCP = OFF_HAB + NBUF * SZ_HAB;
     static constexpr int LDS_BYTES = OFF_RCP + SZ_RCP;
     // item -> thread placement: heavy phases on different waves (see C0 / C1)
     static constexpr int T3 = NT - N3;  // first thread of the P3 items (the top N3 threads)
@@ -589,6 +593,11 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     float2* const Lab = reinterpret_cast<float2*>(smem + C::OFF_LAB);
     float2* const Hab = reinterpret_cast<float2*>(smem + C::OFF_HAB);
     float* const rcp_tab = reinterpret_cast<float*>(smem + C::OFF_RCP);
+    // buffer hb of each hand-off (GF_ONEBAR: two copies, alternating by step parity)
+    auto HxB = [&](auto hbc) { return reinterpret_cast<SA*>(smem + C::OFF_HX + decltype(hbc)::value * C::SZ_HX); };
+    auto LabB = [&](auto hbc) { return reinterpret_cast<float2*>(smem + C::OFF_LAB + decltype(hbc)::value * C::SZ_LAB); };
+    auto HabB = [&](auto hbc) { return reinterpret_cast<float2*>(smem + C::OFF_HAB + decltype(hbc)::value * C::SZ_HAB); };
+    (void)Hx; (void)Lab; (void)Hab;
     // Correctly rounded reciprocals of every possible window count, for div_by_count
     // (Markstein's correction needs RN(1/c) exactly). Published by the prologue's barrier.
     for (int c = threadIdx.x; c <= C::W3; c += NT) rcp_tab[c] = c > 0 ? 1.0f / (float)c : 0.0f;
@@ -766,9 +775,10 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     // P12: z-window of v (f64, running) and its x-window sums on the E2 apron -> Hx. The x
     // neighbours come from the adjacent lanes' quads by DPP wave shifts (whole rows per wave),
     // so the z-window never goes through LDS.
-    auto do_p12 = [&](int tid, auto slotc, auto bc) {
+    auto do_p12 = [&](int tid, auto slotc, auto bc, auto hbc) {
         constexpr int sl = decltype(slotc)::value;  // P1 ring slot of this step
         constexpr int b = decltype(bc)::value;      // prefetch buffer of this step
+        SA* const Hx = HxB(hbc);
 #pragma unroll
         for (int k = 0; k < C::NQP1; ++k) {
             int row, cq;
@@ -870,7 +880,8 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     // every P3 segment lies inside the apron: unconditional Lab stores (a guard lets the compiler
     // sink the second pair's pointwise chain into it, serialising the pairs)
     constexpr bool kRowsWhole = C::E1Y % C::K3 == 0;
-    auto p3_load = [&](int tid, SA (&vin)[C::K3 + 2 * R]) {  // P3's Hx column segment
+    auto p3_load = [&](int tid, SA (&vin)[C::K3 + 2 * R], auto hbc) {  // P3's Hx column segment
+        const SA* const Hx = HxB(hbc);
         const int item = tid - C::T3;
         if (item < 0) return;
         const int col = item % C::E1X, sg = item / C::E1X;
@@ -878,7 +889,8 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
 #pragma unroll
         for (int j = 0; j < C::K3 + 2 * R; ++j) vin[j] = src[j * C::PH];
     };
-    auto do_p3 = [&](int tid, int zc, const SA (&vin)[C::K3 + 2 * R]) {
+    auto do_p3 = [&](int tid, int zc, const SA (&vin)[C::K3 + 2 * R], auto hbc) {
+        float2* const Lab = LabB(hbc);
         // y-window (f64) of Hx -> U; a, b -> Lab
         const int item = tid - C::T3;
         if (item < 0) return;
@@ -936,7 +948,9 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
             }
         }
     };
-    auto do_p4 = [&](int tid) {  // x-window sums of (a, b) rows -> Hab
+    auto do_p4 = [&](int tid, auto hbc) {  // x-window sums of (a, b) rows -> Hab
+        const float2* const Lab = LabB(hbc);
+        float2* const Hab = HabB(hbc);
         const int item = tid;
 #if GF_WAVE_SKIP
         // whole waves past the items branch around the phase (scalar test): exec-masked they
@@ -970,7 +984,8 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     // position P of block B+1 is suffix_B(P+1) + prefix_{B+1}(P). ~3 packed adds per output
     // instead of an f64 running sum (10 ops).
     rsrc_t ro5;  // the output slice P5 stores to this step
-    auto p5_load = [&](int tid, f2 (&vin)[K5 + 2 * R]) {  // P5's Hab column segment
+    auto p5_load = [&](int tid, f2 (&vin)[K5 + 2 * R], auto hbc) {  // P5's Hab column segment
+        const float2* const Hab = HabB(hbc);
         const int col5 = tid % TX, seg5 = tid / TX;
         const f2* src = reinterpret_cast<const f2*>(Hab) + (seg5 * K5) * C::PB + col5;
 #pragma unroll
@@ -1063,7 +1078,7 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     using BL = std::integral_constant<int, PF - 1>;
     load_p1(BL{}, slice_rsrc(zc_begin + R), slice_rsrc(zc_begin - R - 1));
     load_p3v(slice_rsrc(zc_begin));
-    do_p12(tid0, std::integral_constant<int, W - 1>{}, BL{});
+    do_p12(tid0, std::integral_constant<int, W - 1>{}, BL{}, B0{});
     load_p1(B0{}, slice_rsrc(zc_begin + 1 + R), slice_rsrc(zc_begin - R));
     if constexpr (PF == 2) load_p1(BL{}, slice_rsrc(zc_begin + 2 + R), slice_rsrc(zc_begin + 1 - R));
     lds_barrier();
@@ -1092,6 +1107,58 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     // from different slices. The step count is padded to a multiple of W, at least one past the
     // last stage-1 slice so that P5 / the store of the last output slice happen inside the loop:
     // no guards inside. Padded steps emit nothing (zo >= zo_end).
+#if GF_ONEBAR
+    // One barrier per step (double-buffered hand-offs, buffer = step parity): step i runs
+    //   P3(i) [Hx[i] -> Lab[i]], P5(i-2) [Hab[i-2] -> out(i-2-R)], the loads of the next step,
+    //   P4(i-1) [Lab[i-1] -> Hab[i-1]], P12(i+1) [-> Hx[i+1]]
+    // every phase reading the buffer the previous step wrote; the step count covers the emit of
+    // out(zo_end - 1) by P5 at step zc_end + 1.
+    {
+        constexpr int UN = 2 * W;  // even (buffer parity), a multiple of W (ring) and PF (<= 2)
+        const int n_steps = (zc_end - zc_begin + 2 + UN - 1) / UN * UN;
+        zs = zc_begin - 2 - R;  // output slice of this step's P5
+        os = (int64_t)(zs - p.oz0) * osstride;
+        for (int i0 = zc_begin; i0 < zc_begin + n_steps; i0 += UN) {
+            static_for<0, UN>([&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                const int i = i0 + k;
+                const int tid = threadIdx.x;
+                using HR = std::integral_constant<int, k & 1>;        // Hx / Lab of slice i, Hab of i-2
+                using HW = std::integral_constant<int, (k + 1) & 1>;  // Hx of i+1, Lab / Hab of i-1
+                ro5 = make_rsrc(out_base + os, (unsigned)(zs - zo_begin) < nzo ? oslice_bytes : 0u);
+                if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(3);
+                {
+                    SA vin3[C::K3 + 2 * R];
+                    p3_load(tid, vin3, HR{});
+                    do_p3(tid, i, vin3, HR{});
+                }
+                if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(1);
+                {
+                    f2 vin5[K5 + 2 * R];
+                    p5_load(tid, vin5, HR{});
+                    do_p5(tid, i - 2, std::integral_constant<int, (k + 2 * W - 2) % W>{}, vin5);
+                }
+                if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(3);
+                load_p3v(rs_in(ob + (int64_t)R * sstride, zb + R));  // P3 slice i+1
+                load_p5v(rs_in(ob - 2 * sstride, zb - 2));            // P5 slice i-1-R
+                do_p4(tid, HW{});
+                using BK = std::integral_constant<int, k % PF>;
+                do_p12(tid, std::integral_constant<int, k % W>{}, BK{}, HW{});
+                if constexpr (PF == 2)  // for P12(i+3): entering slice i+3+R, leaving i+2-R
+                    load_p1(BK{}, rs_in(ob + off_a + sstride, zb + 2 * R + 2), rs_in(ob + sstride, zb + 1));
+                else
+                    load_p1(BK{}, rs_in(ob + off_a, zb + 2 * R + 1), rs_in(ob, zb));
+                if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(1);
+                lds_barrier();
+                ++zb;
+                ob += sstride;
+                ++zs;
+                os += osstride;
+            });
+        }
+        return;
+    }
+#endif
     constexpr int UN = PF * W;  // unrolled steps: every ring slot and prefetch buffer a constant
     const int n_steps = (zc_end - zc_begin + 1 + UN - 1) / UN * UN;
     for (int i0 = zc_begin; i0 < zc_begin + n_steps; i0 += UN) {
@@ -1115,18 +1182,18 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
                 // as P5 then P3, so each SIMD pairs the LDS-read head of one phase with the VALU
                 // body of the other (P3(i) and P5(i-1) are independent)
                 f2 vin5[K5 + 2 * R];
-                p5_load(tid, vin5);
+                p5_load(tid, vin5, B0{});
                 do_p5(tid, i - 1, std::integral_constant<int, (k + W - 1) % W>{}, vin5);
                 SA vin3[C::K3 + 2 * R];
-                p3_load(tid, vin3);
-                do_p3(tid, i, vin3);
+                p3_load(tid, vin3, B0{});
+                do_p3(tid, i, vin3, B0{});
             } else {
                 SA vin3[C::K3 + 2 * R];
-                p3_load(tid, vin3);
-                do_p3(tid, i, vin3);
+                p3_load(tid, vin3, B0{});
+                do_p3(tid, i, vin3, B0{});
                 if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(1);
                 f2 vin5[K5 + 2 * R];
-                p5_load(tid, vin5);
+                p5_load(tid, vin5, B0{});
                 do_p5(tid, i - 1, std::integral_constant<int, (k + W - 1) % W>{}, vin5);
             }
             lds_barrier();
@@ -1135,15 +1202,15 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
             // issued a step ago.
             load_p3v(rs_in(ob + (int64_t)R * sstride, zb + R));  // P3 slice i+1
             load_p5v(rs_in(ob - sstride, zb - 1));                // P5 slice i-R
-            if constexpr (C::ORDER & 2) do_p4(tid);
+            if constexpr (C::ORDER & 2) do_p4(tid, B0{});
             using BK = std::integral_constant<int, k % PF>;
-            do_p12(tid, std::integral_constant<int, k % W>{}, BK{});
+            do_p12(tid, std::integral_constant<int, k % W>{}, BK{}, B0{});
             if constexpr (PF == 2)  // for P12(i+3): entering slice i+3+R, leaving i+2-R
                 load_p1(BK{}, rs_in(ob + off_a + sstride, zb + 2 * R + 2), rs_in(ob + sstride, zb + 1));
             else
                 load_p1(BK{}, rs_in(ob + off_a, zb + 2 * R + 1), r_b);
             if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(1);
-            if constexpr (!(C::ORDER & 2)) do_p4(tid);
+            if constexpr (!(C::ORDER & 2)) do_p4(tid, B0{});
             lds_barrier();
             ++zb;
             ob += sstride;
