@@ -49,6 +49,9 @@
 #ifndef GF_P1PFD_R2
 #define GF_P1PFD_R2 2  // the same at r <= 2 (stage-1 ring: entering quads only)
 #endif
+#ifndef GF_SOFF
+#define GF_SOFF 0  // per-block descriptors with per-slice soffsets where a block's slices are all inside
+#endif
 #ifndef GF_ONEBAR
 #define GF_ONEBAR 0  // double-buffered Hx / Lab / Hab, one barrier per z-step (see the march)
 #endif
@@ -350,37 +353,37 @@ __device__ __forceinline__ rsrc_t make_rsrc(const void* base, uint32_t bytes) {
 template <typename T> struct Buf;
 template <> struct Buf<float> {
     template <int AUX = 0>
-    __device__ static float load(rsrc_t r, int off) {
-        return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, AUX));
+    __device__ static float load(rsrc_t r, int off, int soff = 0) {
+        return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, soff, AUX));
     }
     // Output stores are streamed with the non-temporal hint (aux 2 = nt) so they do not evict
     // the input slices the march re-reads from L2 a few steps later.
-    __device__ static void store(float v, rsrc_t r, int off) {
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, off, 0, GF_OUT_AUX);
+    __device__ static void store(float v, rsrc_t r, int off, int soff = 0) {
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, off, soff, GF_OUT_AUX);
     }
 };
 template <> struct Buf<uint16_t> {
     template <int AUX = 0>
-    __device__ static float load(rsrc_t r, int off) {
-        return (float)(uint16_t)__builtin_amdgcn_raw_buffer_load_b16(r, off, 0, AUX);
+    __device__ static float load(rsrc_t r, int off, int soff = 0) {
+        return (float)(uint16_t)__builtin_amdgcn_raw_buffer_load_b16(r, off, soff, AUX);
     }
-    __device__ static int load_int(rsrc_t r, int off) {
-        return (int)(uint16_t)__builtin_amdgcn_raw_buffer_load_b16(r, off, 0, 0);
+    __device__ static int load_int(rsrc_t r, int off, int soff = 0) {
+        return (int)(uint16_t)__builtin_amdgcn_raw_buffer_load_b16(r, off, soff, 0);
     }
-    __device__ static void store(uint16_t v, rsrc_t r, int off) {
-        __builtin_amdgcn_raw_buffer_store_b16(v, r, off, 0, 2);
+    __device__ static void store(uint16_t v, rsrc_t r, int off, int soff = 0) {
+        __builtin_amdgcn_raw_buffer_store_b16(v, r, off, soff, 2);
     }
 };
 template <> struct Buf<uint8_t> {
     template <int AUX = 0>
-    __device__ static float load(rsrc_t r, int off) {
-        return (float)(uint8_t)__builtin_amdgcn_raw_buffer_load_b8(r, off, 0, AUX);
+    __device__ static float load(rsrc_t r, int off, int soff = 0) {
+        return (float)(uint8_t)__builtin_amdgcn_raw_buffer_load_b8(r, off, soff, AUX);
     }
-    __device__ static int load_int(rsrc_t r, int off) {
-        return (int)(uint8_t)__builtin_amdgcn_raw_buffer_load_b8(r, off, 0, 0);
+    __device__ static int load_int(rsrc_t r, int off, int soff = 0) {
+        return (int)(uint8_t)__builtin_amdgcn_raw_buffer_load_b8(r, off, soff, 0);
     }
-    __device__ static void store(uint8_t v, rsrc_t r, int off) {
-        __builtin_amdgcn_raw_buffer_store_b8(v, r, off, 0, 2);
+    __device__ static void store(uint8_t v, rsrc_t r, int off, int soff = 0) {
+        __builtin_amdgcn_raw_buffer_store_b8(v, r, off, soff, 2);
     }
 };
 
@@ -411,8 +414,8 @@ typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 template <typename T> struct Quad;
 template <> struct Quad<float> {
     template <int AUX = 0>
-    __device__ static void load(rsrc_t r, int off, float (&v)[4]) {
-        const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, AUX);
+    __device__ static void load(rsrc_t r, int off, float (&v)[4], int soff = 0) {
+        const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(r, off, soff, AUX);
         // (not __builtin_bit_cast on q.y: clang reads element 0 for a bit_cast of a vector
         //  element lvalue)
         v[0] = __uint_as_float(q.x); v[1] = __uint_as_float(q.y);
@@ -426,13 +429,13 @@ template <> struct Quad<float> {
 };
 template <> struct Quad<uint16_t> {
     template <int AUX = 0>
-    __device__ static void load(rsrc_t r, int off, float (&v)[4]) {
-        const u32x2 q = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, AUX);
+    __device__ static void load(rsrc_t r, int off, float (&v)[4], int soff = 0) {
+        const u32x2 q = __builtin_amdgcn_raw_buffer_load_b64(r, off, soff, AUX);
         v[0] = (float)(q.x & 0xffffu); v[1] = (float)(q.x >> 16);
         v[2] = (float)(q.y & 0xffffu); v[3] = (float)(q.y >> 16);
     }
-    __device__ static void load(rsrc_t r, int off, int (&v)[4]) {
-        const u32x2 q = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+    __device__ static void load(rsrc_t r, int off, int (&v)[4], int soff = 0) {
+        const u32x2 q = __builtin_amdgcn_raw_buffer_load_b64(r, off, soff, 0);
         v[0] = (int)(q.x & 0xffffu); v[1] = (int)(q.x >> 16);
         v[2] = (int)(q.y & 0xffffu); v[3] = (int)(q.y >> 16);
     }
@@ -444,13 +447,13 @@ template <> struct Quad<uint16_t> {
 };
 template <> struct Quad<uint8_t> {
     template <int AUX = 0>
-    __device__ static void load(rsrc_t r, int off, float (&v)[4]) {
-        const uint32_t q = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, AUX);
+    __device__ static void load(rsrc_t r, int off, float (&v)[4], int soff = 0) {
+        const uint32_t q = __builtin_amdgcn_raw_buffer_load_b32(r, off, soff, AUX);
         v[0] = (float)(q & 0xffu); v[1] = (float)((q >> 8) & 0xffu);
         v[2] = (float)((q >> 16) & 0xffu); v[3] = (float)(q >> 24);
     }
-    __device__ static void load(rsrc_t r, int off, int (&v)[4]) {
-        const uint32_t q = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
+    __device__ static void load(rsrc_t r, int off, int (&v)[4], int soff = 0) {
+        const uint32_t q = __builtin_amdgcn_raw_buffer_load_b32(r, off, soff, 0);
         v[0] = (int)(q & 0xffu); v[1] = (int)((q >> 8) & 0xffu);
         v[2] = (int)((q >> 16) & 0xffu); v[3] = (int)(q >> 24);
     }
@@ -690,9 +693,9 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
         q1mask[k] = m;
         q1off[k] = (EDGE ? valid : m == 0xF) ? (gy * sy + gx) * ESZ : kBadOff;
     }
-    auto load_quad = [&](rsrc_t r, int off, int mask, SI (&v)[4]) {
-        if constexpr (EDGE) load_quad_masked<TIn>(r, off, mask, v);
-        else Quad<TIn>::load(r, off, v);
+    auto load_quad = [&](rsrc_t r, int off, int mask, SI (&v)[4], int soff = 0) {
+        if constexpr (EDGE) load_quad_masked<TIn>(r, off, mask, v);  // (soff = 0 there)
+        else Quad<TIn>::load(r, off, v, soff);
     };
 
     SA zv[C::NQP1][EPL];
@@ -758,13 +761,13 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     float v5[K5];     // v of the next P5 output slice at this thread's outputs
 #pragma unroll
     for (int j = 0; j < K5; ++j) v5[j] = 0.0f;
-    auto load_p1 = [&](auto bc, rsrc_t ra, rsrc_t rs) {  // entering zc+R, leaving zc-R-1
+    auto load_p1 = [&](auto bc, rsrc_t ra, rsrc_t rs, int sa = 0, int ss = 0) {  // entering zc+R, leaving zc-R-1
         constexpr int b = decltype(bc)::value;
 #pragma unroll
         for (int k = 0; k < C::NQP1; ++k) {
             SI a4[4], s4[4];
-            load_quad(ra, q1off[k], q1mask[k], a4);
-            if constexpr (!C::P1RING) load_quad(rs, q1off[k], q1mask[k], s4);
+            load_quad(ra, q1off[k], q1mask[k], a4, sa);
+            if constexpr (!C::P1RING) load_quad(rs, q1off[k], q1mask[k], s4, ss);
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 pa[b][k][e] = a4[e];
@@ -983,7 +986,8 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     // slice, when it is turned into the suffix sum over [P, W) in place; a window ending at
     // position P of block B+1 is suffix_B(P+1) + prefix_{B+1}(P). ~3 packed adds per output
     // instead of an f64 running sum (10 ops).
-    rsrc_t ro5;  // the output slice P5 stores to this step
+    rsrc_t ro5;    // the output slice P5 stores to this step
+    int so5 = 0;   // and its soffset (GF_SOFF blocks: one descriptor per block of steps)
     auto p5_load = [&](int tid, f2 (&vin)[K5 + 2 * R], auto hbc) {  // P5's Hab column segment
         const float2* const Hab = HabB(hbc);
         const int col5 = tid % TX, seg5 = tid / TX;
@@ -1038,7 +1042,7 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
             const float o = __fadd_rn(__fmul_rn(v5[j], q.x), q.y);  // v*=ma; v+=mb
             const int off = (ox < ox_end && oy < oy_end)
                                 ? ((oy - p.oy0) * osy + (ox - p.ox0)) * OSZ : kBadOff;
-            Buf<TOut>::store(from_f32<TOut>(o), ro5, opaque(off));
+            Buf<TOut>::store(from_f32<TOut>(o), ro5, opaque(off), so5);
         }
     };
 
@@ -1050,7 +1054,7 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     // kernel); straight-line, it waits for exactly the step-old load it needs.
     // Positions outside the domain either read 0 through the range check or read a neighbour
     // row's value that is never used (P3 zeroes its out-of-domain (a, b); P5's store drops).
-    auto load_p3v = [&](rsrc_t r) {
+    auto load_p3v = [&](rsrc_t r, int soff = 0) {
         const int item = (int)threadIdx.x - C::T3;
         const int col = item % C::E1X, sg = item / C::E1X;
         const int gx = x0 - R + col, gy0 = y0 - R + sg * C::K3;
@@ -1058,18 +1062,20 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
         for (int k = 0; k < C::K3; ++k) {
             const int gy = gy0 + k;
             bool ok = item >= 0;
-            if constexpr (EDGE) ok = ok && (unsigned)gx < (unsigned)nx && (unsigned)gy < (unsigned)ny;
-            vc[k] = Buf<TIn>::load(r, opaque(ok ? (gy * sy + gx) * ESZ : kBadOff));
+            // (EDGE, and the soffset streams, whose block descriptor spans several slices: an
+            //  out-of-domain position must not address a neighbouring slice or row, so it reads 0)
+            if constexpr (EDGE || GF_SOFF) ok = ok && (unsigned)gx < (unsigned)nx && (unsigned)gy < (unsigned)ny;
+            vc[k] = Buf<TIn>::load(r, opaque(ok ? (gy * sy + gx) * ESZ : kBadOff), soff);
         }
     };
-    auto load_p5v = [&](rsrc_t r) {
+    auto load_p5v = [&](rsrc_t r, int soff = 0) {
         const int col5 = (int)threadIdx.x % TX, seg5 = (int)threadIdx.x / TX;
         const int ox = x0 + col5, oyb = y0 + seg5 * K5;
 #pragma unroll
         for (int j = 0; j < K5; ++j) {
             const int oy = oyb + j;
             const bool ok = ox < ox_end && oy < oy_end;
-            v5[j] = Buf<TIn>::load(r, opaque(ok ? (oy * sy + ox) * ESZ : kBadOff));
+            v5[j] = Buf<TIn>::load(r, opaque(ok ? (oy * sy + ox) * ESZ : kBadOff), soff);
         }
     };
 
@@ -1095,6 +1101,7 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     int64_t os = (int64_t)(zs - p.oz0) * osstride;
     const char* out_base = static_cast<const char*>(p.out);
     const unsigned nzo = (unsigned)(zo_end - zo_begin);
+    auto rin_null = [&]() { return make_rsrc(in_base, 0u); };
     auto rs_in = [&](int64_t off, int z) {
         return make_rsrc(in_base + off, (unsigned)(z - zlo) < (unsigned)zspan ? slice_bytes : 0u);
     };
@@ -1161,62 +1168,108 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
 #endif
     constexpr int UN = PF * W;  // unrolled steps: every ring slot and prefetch buffer a constant
     const int n_steps = (zc_end - zc_begin + 1 + UN - 1) / UN * UN;
-    for (int i0 = zc_begin; i0 < zc_begin + n_steps; i0 += UN) {
-        static_for<0, UN>([&](auto kc) {
-            constexpr int k = decltype(kc)::value;
-            const int i = i0 + k;
-            const int tid = threadIdx.x;
-            const rsrc_t r_b = rs_in(ob, zb);
+    // A step addresses its slices either through per-slice descriptors (FAST = false: each
+    // descriptor's record count is 0 for a slice outside [zlo, zhi) or an output slice outside
+    // the segment, the zero / dropped slices of the clamped windows) or (FAST = true, a block of
+    // UN steps whose every slice is inside) through one input and one output descriptor per block
+    // with the slice's byte offset in the instruction's SGPR soffset (the hardware range check
+    // covers voffset + soffset: kBadOff lanes still read 0 and drop). The fast form replaces the
+    // 64-bit base arithmetic, range tests and descriptor assembly of five streams per step with
+    // one soffset each.
+    auto step = [&](auto kc, auto fastc, int i0, rsrc_t rin, rsrc_t rout) {
+        constexpr int k = decltype(kc)::value;
+        constexpr bool FAST = decltype(fastc)::value;
+        const int i = i0 + k;
+        const int tid = threadIdx.x;
+        const int ss = (int)sstride, oss = (int)osstride;  // (FAST: spans < 2 GiB)
+        if constexpr (FAST) {
+            ro5 = rout;
+            so5 = (unsigned)(zs - zo_begin) < nzo ? k * oss : 0x7FFFFFF0;  // dropped past records
+        } else {
             ro5 = make_rsrc(out_base + os, (unsigned)(zs - zo_begin) < nzo ? oslice_bytes : 0u);
-            // Fair progress across the waves of a SIMD: the hardware issues oldest-first, which
-            // staggers the waves so the youngest runs its last phase alone, latency exposed. A
-            // wave drops its priority as it completes a phase, so laggards catch up.
-            if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(3);
-            // C0: P3(i) + P5(i-1) (LDS and registers only). P5 runs unconditionally, so no
-            // branch separates its stores from the loads waited on later (the first call's slice
-            // lies in no emitted window, and its stores go to a zero-record descriptor)
-            // (each phase's LDS reads issued right before its arithmetic: hoisting P5's, or both
-            //  phases', ahead of P3 measured +1-4 %, profiles/r05_c0_hoist.txt)
-            if (GF_STAGGER && __builtin_amdgcn_readfirstlane(tid >> 6) >= 8) {
-                // stagger (MI355X_MICROARCH.md "Two waves per SIMD", item 9): waves 8-15 run C0
-                // as P5 then P3, so each SIMD pairs the LDS-read head of one phase with the VALU
-                // body of the other (P3(i) and P5(i-1) are independent)
-                f2 vin5[K5 + 2 * R];
-                p5_load(tid, vin5, B0{});
-                do_p5(tid, i - 1, std::integral_constant<int, (k + W - 1) % W>{}, vin5);
-                SA vin3[C::K3 + 2 * R];
-                p3_load(tid, vin3, B0{});
-                do_p3(tid, i, vin3, B0{});
-            } else {
-                SA vin3[C::K3 + 2 * R];
-                p3_load(tid, vin3, B0{});
-                do_p3(tid, i, vin3, B0{});
-                if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(1);
-                f2 vin5[K5 + 2 * R];
-                p5_load(tid, vin5, B0{});
-                do_p5(tid, i - 1, std::integral_constant<int, (k + W - 1) % W>{}, vin5);
-            }
-            lds_barrier();
-            if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(3);
-            // C1: the loads of the next step, P12(i+1), P4(i). Every wait here is for a load
-            // issued a step ago.
+            so5 = 0;
+        }
+        // Fair progress across the waves of a SIMD: the hardware issues oldest-first, which
+        // staggers the waves so the youngest runs its last phase alone, latency exposed. A
+        // wave drops its priority as it completes a phase, so laggards catch up.
+        if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(3);
+        // C0: P3(i) + P5(i-1) (LDS and registers only). P5 runs unconditionally, so no
+        // branch separates its stores from the loads waited on later (the first call's slice
+        // lies in no emitted window, and its stores go to a zero-record descriptor)
+        // (each phase's LDS reads issued right before its arithmetic: hoisting P5's, or both
+        //  phases', ahead of P3 measured +1-4 %, profiles/r05_c0_hoist.txt)
+        if (GF_STAGGER && __builtin_amdgcn_readfirstlane(tid >> 6) >= 8) {
+            // stagger (MI355X_MICROARCH.md "Two waves per SIMD", item 9): waves 8-15 run C0
+            // as P5 then P3 (round 6: slower)
+            f2 vin5[K5 + 2 * R];
+            p5_load(tid, vin5, B0{});
+            do_p5(tid, i - 1, std::integral_constant<int, (k + W - 1) % W>{}, vin5);
+            SA vin3[C::K3 + 2 * R];
+            p3_load(tid, vin3, B0{});
+            do_p3(tid, i, vin3, B0{});
+        } else {
+            SA vin3[C::K3 + 2 * R];
+            p3_load(tid, vin3, B0{});
+            do_p3(tid, i, vin3, B0{});
+            if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(1);
+            f2 vin5[K5 + 2 * R];
+            p5_load(tid, vin5, B0{});
+            do_p5(tid, i - 1, std::integral_constant<int, (k + W - 1) % W>{}, vin5);
+        }
+        lds_barrier();
+        if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(3);
+        // C1: the loads of the next step, P12(i+1), P4(i). Every wait here is for a load
+        // issued a step ago.
+        using BK = std::integral_constant<int, k % PF>;
+        // FAST: rin's base is slice zb0 - 1 of the block, so slice zb + d sits at soffset
+        // (k + d + 1) * ss; a slice outside [zlo, zhi) gets a soffset past the records (reads 0)
+        auto sin = [&](int d, int so) {
+            return (unsigned)(zb + d - zlo) < (unsigned)zspan ? so : 0x7FFFFFF0;
+        };
+        if constexpr (FAST) {
+            load_p3v(rin, sin(R, (k + R + 1) * ss));  // P3 slice i+1 = zb + R
+            load_p5v(rin, sin(-1, k * ss));           // P5 slice i-R = zb - 1
+        } else {
             load_p3v(rs_in(ob + (int64_t)R * sstride, zb + R));  // P3 slice i+1
             load_p5v(rs_in(ob - sstride, zb - 1));                // P5 slice i-R
-            if constexpr (C::ORDER & 2) do_p4(tid, B0{});
-            using BK = std::integral_constant<int, k % PF>;
-            do_p12(tid, std::integral_constant<int, k % W>{}, BK{}, B0{});
+        }
+        if constexpr (C::ORDER & 2) do_p4(tid, B0{});
+        do_p12(tid, std::integral_constant<int, k % W>{}, BK{}, B0{});
+        if constexpr (FAST) {
+            if constexpr (PF == 2)  // entering zb + 2R + 2, leaving zb + 1
+                load_p1(BK{}, rin, rin, sin(2 * R + 2, (k + 2 * R + 3) * ss), sin(1, (k + 2) * ss));
+            else  // entering zb + 2R + 1, leaving zb
+                load_p1(BK{}, rin, rin, sin(2 * R + 1, (k + 2 * R + 2) * ss), sin(0, (k + 1) * ss));
+        } else {
             if constexpr (PF == 2)  // for P12(i+3): entering slice i+3+R, leaving i+2-R
                 load_p1(BK{}, rs_in(ob + off_a + sstride, zb + 2 * R + 2), rs_in(ob + sstride, zb + 1));
             else
-                load_p1(BK{}, rs_in(ob + off_a, zb + 2 * R + 1), r_b);
-            if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(1);
-            if constexpr (!(C::ORDER & 2)) do_p4(tid, B0{});
-            lds_barrier();
-            ++zb;
-            ob += sstride;
-            ++zs;
-            os += osstride;
-        });
+                load_p1(BK{}, rs_in(ob + off_a, zb + 2 * R + 1), rs_in(ob, zb));
+        }
+        if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(1);
+        if constexpr (!(C::ORDER & 2)) do_p4(tid, B0{});
+        lds_barrier();
+        ++zb;
+        ob += sstride;
+        ++zs;
+        os += osstride;
+    };
+    // a block of UN steps reads slices [zb - 1, zb + UN + 2R + 1] (PF = 2; one less at PF = 1)
+    const int64_t in_span = (int64_t)(UN + 2 * R + 3) * sstride;
+    const int64_t out_span = (int64_t)UN * osstride;
+    const bool fast = GF_SOFF && !EDGE && in_span < ((int64_t)1 << 31) &&
+                      out_span < ((int64_t)1 << 31);
+    if (GF_SOFF == 2 || fast) {  // 2: the fast form only (the host checks the spans)
+        for (int i0 = zc_begin; i0 < zc_begin + n_steps; i0 += UN) {
+            // the block's base slice zb - 1 may lie outside the array: its slices then never
+            // address memory (their soffset is past the records)
+            const rsrc_t rin = make_rsrc(in_base + ob - sstride, (uint32_t)in_span);
+            const rsrc_t rout = make_rsrc(out_base + os, (uint32_t)out_span);
+            static_for<0, UN>([&](auto kc) { step(kc, std::true_type{}, i0, rin, rout); });
+        }
+    } else if constexpr (GF_SOFF != 2) {
+        for (int i0 = zc_begin; i0 < zc_begin + n_steps; i0 += UN)
+            static_for<0, UN>([&](auto kc) { step(kc, std::false_type{}, i0, rin_null(), rin_null()); });
     }
 }
 
