@@ -10,7 +10,7 @@
 #include <cstdlib>
 #include <vector>
 
-#include "../zarrs_tools_amd/csrc/gf_role.hpp"
+#include "../zarrs_tools_amd/csrc/gf_fused.hpp"
 
 using namespace zt;
 #ifndef TK_TY
@@ -30,7 +30,7 @@ using TIN = float;
 #endif
 
 #ifndef TK_LAUNCH
-#define TK_LAUNCH 0  // 0: launch_fused_cfg; 9: gf3d_role_kernel; 1: mode 1 over every tile; 2: mode 0 over every tile
+#define TK_LAUNCH 0  // 0: launch_fused_cfg; 1: mode 1 over every tile; 2: mode 0 over every tile
                      // (timing only: the border tiles' output is wrong)
 #endif
 
@@ -66,7 +66,6 @@ int main(int argc, char** argv) {
     hipStream_t s; CK(hipStreamCreate(&s));
     auto launch = [&](const GFParams& p0, hipStream_t st) -> hipError_t {
         if (TK_LAUNCH == 0) return launch_fused_cfg<TK_R, TK_TY, TK_NT, TIN, float>(p0, st);
-        if (TK_LAUNCH == 9) return launch_role<TK_R, TIN, float>(p0, st);  // role-split kernel
         using C = GFConfig<TK_R, TK_TY, TK_NT>;
         GFParams q = p0;
         volatile float one = 1.0f;

@@ -49,15 +49,6 @@
 #ifndef GF_P1PFD_R2
 #define GF_P1PFD_R2 2  // the same at r <= 2 (stage-1 ring: entering quads only)
 #endif
-#ifndef GF_SOFF
-#define GF_SOFF 0  // per-block descriptors with per-slice soffsets where a block's slices are all inside
-#endif
-#ifndef GF_ONEBAR
-#define GF_ONEBAR 0  // double-buffered Hx / Lab / Hab, one barrier per z-step (see the march)
-#endif
-#ifndef GF_STAGGER
-#define GF_STAGGER 0  // C0 phase order P5, P3 on waves 8-15 (P3, P5 on waves 0-7)
-#endif
 #ifndef GF_WAVE_SKIP
 #define GF_WAVE_SKIP 1  // P4: idle waves branch around the phase
 #endif
@@ -353,37 +344,37 @@ __device__ __forceinline__ rsrc_t make_rsrc(const void* base, uint32_t bytes) {
 template <typename T> struct Buf;
 template <> struct Buf<float> {
     template <int AUX = 0>
-    __device__ static float load(rsrc_t r, int off, int soff = 0) {
-        return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, soff, AUX));
+    __device__ static float load(rsrc_t r, int off) {
+        return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, AUX));
     }
     // Output stores are streamed with the non-temporal hint (aux 2 = nt) so they do not evict
     // the input slices the march re-reads from L2 a few steps later.
-    __device__ static void store(float v, rsrc_t r, int off, int soff = 0) {
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, off, soff, GF_OUT_AUX);
+    __device__ static void store(float v, rsrc_t r, int off) {
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, off, 0, GF_OUT_AUX);
     }
 };
 template <> struct Buf<uint16_t> {
     template <int AUX = 0>
-    __device__ static float load(rsrc_t r, int off, int soff = 0) {
-        return (float)(uint16_t)__builtin_amdgcn_raw_buffer_load_b16(r, off, soff, AUX);
+    __device__ static float load(rsrc_t r, int off) {
+        return (float)(uint16_t)__builtin_amdgcn_raw_buffer_load_b16(r, off, 0, AUX);
     }
-    __device__ static int load_int(rsrc_t r, int off, int soff = 0) {
-        return (int)(uint16_t)__builtin_amdgcn_raw_buffer_load_b16(r, off, soff, 0);
+    __device__ static int load_int(rsrc_t r, int off) {
+        return (int)(uint16_t)__builtin_amdgcn_raw_buffer_load_b16(r, off, 0, 0);
     }
-    __device__ static void store(uint16_t v, rsrc_t r, int off, int soff = 0) {
-        __builtin_amdgcn_raw_buffer_store_b16(v, r, off, soff, 2);
+    __device__ static void store(uint16_t v, rsrc_t r, int off) {
+        __builtin_amdgcn_raw_buffer_store_b16(v, r, off, 0, 2);
     }
 };
 template <> struct Buf<uint8_t> {
     template <int AUX = 0>
-    __device__ static float load(rsrc_t r, int off, int soff = 0) {
-        return (float)(uint8_t)__builtin_amdgcn_raw_buffer_load_b8(r, off, soff, AUX);
+    __device__ static float load(rsrc_t r, int off) {
+        return (float)(uint8_t)__builtin_amdgcn_raw_buffer_load_b8(r, off, 0, AUX);
     }
-    __device__ static int load_int(rsrc_t r, int off, int soff = 0) {
-        return (int)(uint8_t)__builtin_amdgcn_raw_buffer_load_b8(r, off, soff, 0);
+    __device__ static int load_int(rsrc_t r, int off) {
+        return (int)(uint8_t)__builtin_amdgcn_raw_buffer_load_b8(r, off, 0, 0);
     }
-    __device__ static void store(uint8_t v, rsrc_t r, int off, int soff = 0) {
-        __builtin_amdgcn_raw_buffer_store_b8(v, r, off, soff, 2);
+    __device__ static void store(uint8_t v, rsrc_t r, int off) {
+        __builtin_amdgcn_raw_buffer_store_b8(v, r, off, 0, 2);
     }
 };
 
@@ -414,8 +405,8 @@ typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 template <typename T> struct Quad;
 template <> struct Quad<float> {
     template <int AUX = 0>
-    __device__ static void load(rsrc_t r, int off, float (&v)[4], int soff = 0) {
-        const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(r, off, soff, AUX);
+    __device__ static void load(rsrc_t r, int off, float (&v)[4]) {
+        const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, AUX);
         // (not __builtin_bit_cast on q.y: clang reads element 0 for a bit_cast of a vector
         //  element lvalue)
         v[0] = __uint_as_float(q.x); v[1] = __uint_as_float(q.y);
@@ -429,13 +420,13 @@ template <> struct Quad<float> {
 };
 template <> struct Quad<uint16_t> {
     template <int AUX = 0>
-    __device__ static void load(rsrc_t r, int off, float (&v)[4], int soff = 0) {
-        const u32x2 q = __builtin_amdgcn_raw_buffer_load_b64(r, off, soff, AUX);
+    __device__ static void load(rsrc_t r, int off, float (&v)[4]) {
+        const u32x2 q = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, AUX);
         v[0] = (float)(q.x & 0xffffu); v[1] = (float)(q.x >> 16);
         v[2] = (float)(q.y & 0xffffu); v[3] = (float)(q.y >> 16);
     }
-    __device__ static void load(rsrc_t r, int off, int (&v)[4], int soff = 0) {
-        const u32x2 q = __builtin_amdgcn_raw_buffer_load_b64(r, off, soff, 0);
+    __device__ static void load(rsrc_t r, int off, int (&v)[4]) {
+        const u32x2 q = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
         v[0] = (int)(q.x & 0xffffu); v[1] = (int)(q.x >> 16);
         v[2] = (int)(q.y & 0xffffu); v[3] = (int)(q.y >> 16);
     }
@@ -447,13 +438,13 @@ template <> struct Quad<uint16_t> {
 };
 template <> struct Quad<uint8_t> {
     template <int AUX = 0>
-    __device__ static void load(rsrc_t r, int off, float (&v)[4], int soff = 0) {
-        const uint32_t q = __builtin_amdgcn_raw_buffer_load_b32(r, off, soff, AUX);
+    __device__ static void load(rsrc_t r, int off, float (&v)[4]) {
+        const uint32_t q = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, AUX);
         v[0] = (float)(q & 0xffu); v[1] = (float)((q >> 8) & 0xffu);
         v[2] = (float)((q >> 16) & 0xffu); v[3] = (float)(q >> 24);
     }
-    __device__ static void load(rsrc_t r, int off, int (&v)[4], int soff = 0) {
-        const uint32_t q = __builtin_amdgcn_raw_buffer_load_b32(r, off, soff, 0);
+    __device__ static void load(rsrc_t r, int off, int (&v)[4]) {
+        const uint32_t q = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
         v[0] = (int)(q & 0xffu); v[1] = (int)((q >> 8) & 0xffu);
         v[2] = (int)((q >> 16) & 0xffu); v[3] = (int)(q >> 24);
     }
@@ -553,10 +544,9 @@ struct GFConfig {
     static constexpr int SZ_LAB = al((E1Y + 1) * PA * 8);
     static constexpr int SZ_HAB = al((E1Y + 1) * PB * 8);
     static constexpr int SZ_RCP = al((W3 + 1) * 4);  // RN(1/c) for window counts c <= W^3
-    static constexpr int NBUF = GF_ONEBAR ? 2 : 1;  // copies of each hand-off buffer
-    static constexpr int OFF_HX = 0, OFF_LAB = OFF_HX + NBUF * SZ_HX;
-    static constexpr int OFF_HAB = OFF_LAB + NBUF * SZ_LAB;
-    static constexpr int OFF_RCP = OFF_HAB + NBUF * SZ_HAB;
+    static constexpr int OFF_HX = 0, OFF_LAB = OFF_HX + SZ_HX;
+    static constexpr int OFF_HAB = OFF_LAB + SZ_LAB;
+    static constexpr int OFF_RCP = OFF_HAB + SZ_HAB;
     static constexpr int LDS_BYTES = OFF_RCP + SZ_RCP;
     // item -> thread placement: heavy phases on different waves (see C0 / C1)
     static constexpr int T3 = NT - N3;  // first thread of the P3 items (the top N3 threads)
@@ -596,11 +586,6 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     float2* const Lab = reinterpret_cast<float2*>(smem + C::OFF_LAB);
     float2* const Hab = reinterpret_cast<float2*>(smem + C::OFF_HAB);
     float* const rcp_tab = reinterpret_cast<float*>(smem + C::OFF_RCP);
-    // buffer hb of each hand-off (GF_ONEBAR: two copies, alternating by step parity)
-    auto HxB = [&](auto hbc) { return reinterpret_cast<SA*>(smem + C::OFF_HX + decltype(hbc)::value * C::SZ_HX); };
-    auto LabB = [&](auto hbc) { return reinterpret_cast<float2*>(smem + C::OFF_LAB + decltype(hbc)::value * C::SZ_LAB); };
-    auto HabB = [&](auto hbc) { return reinterpret_cast<float2*>(smem + C::OFF_HAB + decltype(hbc)::value * C::SZ_HAB); };
-    (void)Hx; (void)Lab; (void)Hab;
     // Correctly rounded reciprocals of every possible window count, for div_by_count
     // (Markstein's correction needs RN(1/c) exactly). Published by the prologue's barrier.
     for (int c = threadIdx.x; c <= C::W3; c += NT) rcp_tab[c] = c > 0 ? 1.0f / (float)c : 0.0f;
@@ -693,9 +678,9 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
         q1mask[k] = m;
         q1off[k] = (EDGE ? valid : m == 0xF) ? (gy * sy + gx) * ESZ : kBadOff;
     }
-    auto load_quad = [&](rsrc_t r, int off, int mask, SI (&v)[4], int soff = 0) {
-        if constexpr (EDGE) load_quad_masked<TIn>(r, off, mask, v);  // (soff = 0 there)
-        else Quad<TIn>::load(r, off, v, soff);
+    auto load_quad = [&](rsrc_t r, int off, int mask, SI (&v)[4]) {
+        if constexpr (EDGE) load_quad_masked<TIn>(r, off, mask, v);
+        else Quad<TIn>::load(r, off, v);
     };
 
     SA zv[C::NQP1][EPL];
@@ -761,13 +746,13 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     float v5[K5];     // v of the next P5 output slice at this thread's outputs
 #pragma unroll
     for (int j = 0; j < K5; ++j) v5[j] = 0.0f;
-    auto load_p1 = [&](auto bc, rsrc_t ra, rsrc_t rs, int sa = 0, int ss = 0) {  // entering zc+R, leaving zc-R-1
+    auto load_p1 = [&](auto bc, rsrc_t ra, rsrc_t rs) {  // entering zc+R, leaving zc-R-1
         constexpr int b = decltype(bc)::value;
 #pragma unroll
         for (int k = 0; k < C::NQP1; ++k) {
             SI a4[4], s4[4];
-            load_quad(ra, q1off[k], q1mask[k], a4, sa);
-            if constexpr (!C::P1RING) load_quad(rs, q1off[k], q1mask[k], s4, ss);
+            load_quad(ra, q1off[k], q1mask[k], a4);
+            if constexpr (!C::P1RING) load_quad(rs, q1off[k], q1mask[k], s4);
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 pa[b][k][e] = a4[e];
@@ -778,10 +763,9 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     // P12: z-window of v (f64, running) and its x-window sums on the E2 apron -> Hx. The x
     // neighbours come from the adjacent lanes' quads by DPP wave shifts (whole rows per wave),
     // so the z-window never goes through LDS.
-    auto do_p12 = [&](int tid, auto slotc, auto bc, auto hbc) {
+    auto do_p12 = [&](int tid, auto slotc, auto bc) {
         constexpr int sl = decltype(slotc)::value;  // P1 ring slot of this step
         constexpr int b = decltype(bc)::value;      // prefetch buffer of this step
-        SA* const Hx = HxB(hbc);
 #pragma unroll
         for (int k = 0; k < C::NQP1; ++k) {
             int row, cq;
@@ -883,8 +867,7 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     // every P3 segment lies inside the apron: unconditional Lab stores (a guard lets the compiler
     // sink the second pair's pointwise chain into it, serialising the pairs)
     constexpr bool kRowsWhole = C::E1Y % C::K3 == 0;
-    auto p3_load = [&](int tid, SA (&vin)[C::K3 + 2 * R], auto hbc) {  // P3's Hx column segment
-        const SA* const Hx = HxB(hbc);
+    auto p3_load = [&](int tid, SA (&vin)[C::K3 + 2 * R]) {  // P3's Hx column segment
         const int item = tid - C::T3;
         if (item < 0) return;
         const int col = item % C::E1X, sg = item / C::E1X;
@@ -892,8 +875,7 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
 #pragma unroll
         for (int j = 0; j < C::K3 + 2 * R; ++j) vin[j] = src[j * C::PH];
     };
-    auto do_p3 = [&](int tid, int zc, const SA (&vin)[C::K3 + 2 * R], auto hbc) {
-        float2* const Lab = LabB(hbc);
+    auto do_p3 = [&](int tid, int zc, const SA (&vin)[C::K3 + 2 * R]) {
         // y-window (f64) of Hx -> U; a, b -> Lab
         const int item = tid - C::T3;
         if (item < 0) return;
@@ -951,9 +933,7 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
             }
         }
     };
-    auto do_p4 = [&](int tid, auto hbc) {  // x-window sums of (a, b) rows -> Hab
-        const float2* const Lab = LabB(hbc);
-        float2* const Hab = HabB(hbc);
+    auto do_p4 = [&](int tid) {  // x-window sums of (a, b) rows -> Hab
         const int item = tid;
 #if GF_WAVE_SKIP
         // whole waves past the items branch around the phase (scalar test): exec-masked they
@@ -986,10 +966,8 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     // slice, when it is turned into the suffix sum over [P, W) in place; a window ending at
     // position P of block B+1 is suffix_B(P+1) + prefix_{B+1}(P). ~3 packed adds per output
     // instead of an f64 running sum (10 ops).
-    rsrc_t ro5;    // the output slice P5 stores to this step
-    int so5 = 0;   // and its soffset (GF_SOFF blocks: one descriptor per block of steps)
-    auto p5_load = [&](int tid, f2 (&vin)[K5 + 2 * R], auto hbc) {  // P5's Hab column segment
-        const float2* const Hab = HabB(hbc);
+    rsrc_t ro5;  // the output slice P5 stores to this step
+    auto p5_load = [&](int tid, f2 (&vin)[K5 + 2 * R]) {  // P5's Hab column segment
         const int col5 = tid % TX, seg5 = tid / TX;
         const f2* src = reinterpret_cast<const f2*>(Hab) + (seg5 * K5) * C::PB + col5;
 #pragma unroll
@@ -1042,7 +1020,7 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
             const float o = __fadd_rn(__fmul_rn(v5[j], q.x), q.y);  // v*=ma; v+=mb
             const int off = (ox < ox_end && oy < oy_end)
                                 ? ((oy - p.oy0) * osy + (ox - p.ox0)) * OSZ : kBadOff;
-            Buf<TOut>::store(from_f32<TOut>(o), ro5, opaque(off), so5);
+            Buf<TOut>::store(from_f32<TOut>(o), ro5, opaque(off));
         }
     };
 
@@ -1054,7 +1032,7 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     // kernel); straight-line, it waits for exactly the step-old load it needs.
     // Positions outside the domain either read 0 through the range check or read a neighbour
     // row's value that is never used (P3 zeroes its out-of-domain (a, b); P5's store drops).
-    auto load_p3v = [&](rsrc_t r, int soff = 0) {
+    auto load_p3v = [&](rsrc_t r) {
         const int item = (int)threadIdx.x - C::T3;
         const int col = item % C::E1X, sg = item / C::E1X;
         const int gx = x0 - R + col, gy0 = y0 - R + sg * C::K3;
@@ -1062,20 +1040,18 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
         for (int k = 0; k < C::K3; ++k) {
             const int gy = gy0 + k;
             bool ok = item >= 0;
-            // (EDGE, and the soffset streams, whose block descriptor spans several slices: an
-            //  out-of-domain position must not address a neighbouring slice or row, so it reads 0)
-            if constexpr (EDGE || GF_SOFF) ok = ok && (unsigned)gx < (unsigned)nx && (unsigned)gy < (unsigned)ny;
-            vc[k] = Buf<TIn>::load(r, opaque(ok ? (gy * sy + gx) * ESZ : kBadOff), soff);
+            if constexpr (EDGE) ok = ok && (unsigned)gx < (unsigned)nx && (unsigned)gy < (unsigned)ny;
+            vc[k] = Buf<TIn>::load(r, opaque(ok ? (gy * sy + gx) * ESZ : kBadOff));
         }
     };
-    auto load_p5v = [&](rsrc_t r, int soff = 0) {
+    auto load_p5v = [&](rsrc_t r) {
         const int col5 = (int)threadIdx.x % TX, seg5 = (int)threadIdx.x / TX;
         const int ox = x0 + col5, oyb = y0 + seg5 * K5;
 #pragma unroll
         for (int j = 0; j < K5; ++j) {
             const int oy = oyb + j;
             const bool ok = ox < ox_end && oy < oy_end;
-            v5[j] = Buf<TIn>::load(r, opaque(ok ? (oy * sy + ox) * ESZ : kBadOff), soff);
+            v5[j] = Buf<TIn>::load(r, opaque(ok ? (oy * sy + ox) * ESZ : kBadOff));
         }
     };
 
@@ -1084,7 +1060,7 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     using BL = std::integral_constant<int, PF - 1>;
     load_p1(BL{}, slice_rsrc(zc_begin + R), slice_rsrc(zc_begin - R - 1));
     load_p3v(slice_rsrc(zc_begin));
-    do_p12(tid0, std::integral_constant<int, W - 1>{}, BL{}, B0{});
+    do_p12(tid0, std::integral_constant<int, W - 1>{}, BL{});
     load_p1(B0{}, slice_rsrc(zc_begin + 1 + R), slice_rsrc(zc_begin - R));
     if constexpr (PF == 2) load_p1(BL{}, slice_rsrc(zc_begin + 2 + R), slice_rsrc(zc_begin + 1 - R));
     lds_barrier();
@@ -1101,7 +1077,6 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     int64_t os = (int64_t)(zs - p.oz0) * osstride;
     const char* out_base = static_cast<const char*>(p.out);
     const unsigned nzo = (unsigned)(zo_end - zo_begin);
-    auto rin_null = [&]() { return make_rsrc(in_base, 0u); };
     auto rs_in = [&](int64_t off, int z) {
         return make_rsrc(in_base + off, (unsigned)(z - zlo) < (unsigned)zspan ? slice_bytes : 0u);
     };
@@ -1114,162 +1089,52 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     // from different slices. The step count is padded to a multiple of W, at least one past the
     // last stage-1 slice so that P5 / the store of the last output slice happen inside the loop:
     // no guards inside. Padded steps emit nothing (zo >= zo_end).
-#if GF_ONEBAR
-    // One barrier per step (double-buffered hand-offs, buffer = step parity): step i runs
-    //   P3(i) [Hx[i] -> Lab[i]], P5(i-2) [Hab[i-2] -> out(i-2-R)], the loads of the next step,
-    //   P4(i-1) [Lab[i-1] -> Hab[i-1]], P12(i+1) [-> Hx[i+1]]
-    // every phase reading the buffer the previous step wrote; the step count covers the emit of
-    // out(zo_end - 1) by P5 at step zc_end + 1.
-    {
-        constexpr int UN = 2 * W;  // even (buffer parity), a multiple of W (ring) and PF (<= 2)
-        const int n_steps = (zc_end - zc_begin + 2 + UN - 1) / UN * UN;
-        zs = zc_begin - 2 - R;  // output slice of this step's P5
-        os = (int64_t)(zs - p.oz0) * osstride;
-        for (int i0 = zc_begin; i0 < zc_begin + n_steps; i0 += UN) {
-            static_for<0, UN>([&](auto kc) {
-                constexpr int k = decltype(kc)::value;
-                const int i = i0 + k;
-                const int tid = threadIdx.x;
-                using HR = std::integral_constant<int, k & 1>;        // Hx / Lab of slice i, Hab of i-2
-                using HW = std::integral_constant<int, (k + 1) & 1>;  // Hx of i+1, Lab / Hab of i-1
-                ro5 = make_rsrc(out_base + os, (unsigned)(zs - zo_begin) < nzo ? oslice_bytes : 0u);
-                if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(3);
-                {
-                    SA vin3[C::K3 + 2 * R];
-                    p3_load(tid, vin3, HR{});
-                    do_p3(tid, i, vin3, HR{});
-                }
-                if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(1);
-                {
-                    f2 vin5[K5 + 2 * R];
-                    p5_load(tid, vin5, HR{});
-                    do_p5(tid, i - 2, std::integral_constant<int, (k + 2 * W - 2) % W>{}, vin5);
-                }
-                if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(3);
-                load_p3v(rs_in(ob + (int64_t)R * sstride, zb + R));  // P3 slice i+1
-                load_p5v(rs_in(ob - 2 * sstride, zb - 2));            // P5 slice i-1-R
-                do_p4(tid, HW{});
-                using BK = std::integral_constant<int, k % PF>;
-                do_p12(tid, std::integral_constant<int, k % W>{}, BK{}, HW{});
-                if constexpr (PF == 2)  // for P12(i+3): entering slice i+3+R, leaving i+2-R
-                    load_p1(BK{}, rs_in(ob + off_a + sstride, zb + 2 * R + 2), rs_in(ob + sstride, zb + 1));
-                else
-                    load_p1(BK{}, rs_in(ob + off_a, zb + 2 * R + 1), rs_in(ob, zb));
-                if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(1);
-                lds_barrier();
-                ++zb;
-                ob += sstride;
-                ++zs;
-                os += osstride;
-            });
-        }
-        return;
-    }
-#endif
     constexpr int UN = PF * W;  // unrolled steps: every ring slot and prefetch buffer a constant
     const int n_steps = (zc_end - zc_begin + 1 + UN - 1) / UN * UN;
-    // A step addresses its slices either through per-slice descriptors (FAST = false: each
-    // descriptor's record count is 0 for a slice outside [zlo, zhi) or an output slice outside
-    // the segment, the zero / dropped slices of the clamped windows) or (FAST = true, a block of
-    // UN steps whose every slice is inside) through one input and one output descriptor per block
-    // with the slice's byte offset in the instruction's SGPR soffset (the hardware range check
-    // covers voffset + soffset: kBadOff lanes still read 0 and drop). The fast form replaces the
-    // 64-bit base arithmetic, range tests and descriptor assembly of five streams per step with
-    // one soffset each.
-    auto step = [&](auto kc, auto fastc, int i0, rsrc_t rin, rsrc_t rout) {
-        constexpr int k = decltype(kc)::value;
-        constexpr bool FAST = decltype(fastc)::value;
-        const int i = i0 + k;
-        const int tid = threadIdx.x;
-        const int ss = (int)sstride, oss = (int)osstride;  // (FAST: spans < 2 GiB)
-        if constexpr (FAST) {
-            ro5 = rout;
-            so5 = (unsigned)(zs - zo_begin) < nzo ? k * oss : 0x7FFFFFF0;  // dropped past records
-        } else {
+    for (int i0 = zc_begin; i0 < zc_begin + n_steps; i0 += UN) {
+        static_for<0, UN>([&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            const int i = i0 + k;
+            const int tid = threadIdx.x;
+            const rsrc_t r_b = rs_in(ob, zb);
             ro5 = make_rsrc(out_base + os, (unsigned)(zs - zo_begin) < nzo ? oslice_bytes : 0u);
-            so5 = 0;
-        }
-        // Fair progress across the waves of a SIMD: the hardware issues oldest-first, which
-        // staggers the waves so the youngest runs its last phase alone, latency exposed. A
-        // wave drops its priority as it completes a phase, so laggards catch up.
-        if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(3);
-        // C0: P3(i) + P5(i-1) (LDS and registers only). P5 runs unconditionally, so no
-        // branch separates its stores from the loads waited on later (the first call's slice
-        // lies in no emitted window, and its stores go to a zero-record descriptor)
-        // (each phase's LDS reads issued right before its arithmetic: hoisting P5's, or both
-        //  phases', ahead of P3 measured +1-4 %, profiles/r05_c0_hoist.txt)
-        if (GF_STAGGER && __builtin_amdgcn_readfirstlane(tid >> 6) >= 8) {
-            // stagger (MI355X_MICROARCH.md "Two waves per SIMD", item 9): waves 8-15 run C0
-            // as P5 then P3 (round 6: slower)
-            f2 vin5[K5 + 2 * R];
-            p5_load(tid, vin5, B0{});
-            do_p5(tid, i - 1, std::integral_constant<int, (k + W - 1) % W>{}, vin5);
+            // Fair progress across the waves of a SIMD: the hardware issues oldest-first, which
+            // staggers the waves so the youngest runs its last phase alone, latency exposed. A
+            // wave drops its priority as it completes a phase, so laggards catch up.
+            if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(3);
+            // C0: P3(i) + P5(i-1) (LDS and registers only). P5 runs unconditionally, so no
+            // branch separates its stores from the loads waited on later (the first call's slice
+            // lies in no emitted window, and its stores go to a zero-record descriptor)
+            // (each phase's LDS reads issued right before its arithmetic: hoisting P5's, or both
+            //  phases', ahead of P3 measured +1-4 %, profiles/r05_c0_hoist.txt)
             SA vin3[C::K3 + 2 * R];
-            p3_load(tid, vin3, B0{});
-            do_p3(tid, i, vin3, B0{});
-        } else {
-            SA vin3[C::K3 + 2 * R];
-            p3_load(tid, vin3, B0{});
-            do_p3(tid, i, vin3, B0{});
+            p3_load(tid, vin3);
+            do_p3(tid, i, vin3);
             if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(1);
             f2 vin5[K5 + 2 * R];
-            p5_load(tid, vin5, B0{});
+            p5_load(tid, vin5);
             do_p5(tid, i - 1, std::integral_constant<int, (k + W - 1) % W>{}, vin5);
-        }
-        lds_barrier();
-        if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(3);
-        // C1: the loads of the next step, P12(i+1), P4(i). Every wait here is for a load
-        // issued a step ago.
-        using BK = std::integral_constant<int, k % PF>;
-        // FAST: rin's base is slice zb0 - 1 of the block, so slice zb + d sits at soffset
-        // (k + d + 1) * ss; a slice outside [zlo, zhi) gets a soffset past the records (reads 0)
-        auto sin = [&](int d, int so) {
-            return (unsigned)(zb + d - zlo) < (unsigned)zspan ? so : 0x7FFFFFF0;
-        };
-        if constexpr (FAST) {
-            load_p3v(rin, sin(R, (k + R + 1) * ss));  // P3 slice i+1 = zb + R
-            load_p5v(rin, sin(-1, k * ss));           // P5 slice i-R = zb - 1
-        } else {
+            lds_barrier();
+            if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(3);
+            // C1: the loads of the next step, P12(i+1), P4(i). Every wait here is for a load
+            // issued a step ago.
             load_p3v(rs_in(ob + (int64_t)R * sstride, zb + R));  // P3 slice i+1
             load_p5v(rs_in(ob - sstride, zb - 1));                // P5 slice i-R
-        }
-        if constexpr (C::ORDER & 2) do_p4(tid, B0{});
-        do_p12(tid, std::integral_constant<int, k % W>{}, BK{}, B0{});
-        if constexpr (FAST) {
-            if constexpr (PF == 2)  // entering zb + 2R + 2, leaving zb + 1
-                load_p1(BK{}, rin, rin, sin(2 * R + 2, (k + 2 * R + 3) * ss), sin(1, (k + 2) * ss));
-            else  // entering zb + 2R + 1, leaving zb
-                load_p1(BK{}, rin, rin, sin(2 * R + 1, (k + 2 * R + 2) * ss), sin(0, (k + 1) * ss));
-        } else {
+            if constexpr (C::ORDER & 2) do_p4(tid);
+            using BK = std::integral_constant<int, k % PF>;
+            do_p12(tid, std::integral_constant<int, k % W>{}, BK{});
             if constexpr (PF == 2)  // for P12(i+3): entering slice i+3+R, leaving i+2-R
                 load_p1(BK{}, rs_in(ob + off_a + sstride, zb + 2 * R + 2), rs_in(ob + sstride, zb + 1));
             else
-                load_p1(BK{}, rs_in(ob + off_a, zb + 2 * R + 1), rs_in(ob, zb));
-        }
-        if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(1);
-        if constexpr (!(C::ORDER & 2)) do_p4(tid, B0{});
-        lds_barrier();
-        ++zb;
-        ob += sstride;
-        ++zs;
-        os += osstride;
-    };
-    // a block of UN steps reads slices [zb - 1, zb + UN + 2R + 1] (PF = 2; one less at PF = 1)
-    const int64_t in_span = (int64_t)(UN + 2 * R + 3) * sstride;
-    const int64_t out_span = (int64_t)UN * osstride;
-    const bool fast = GF_SOFF && !EDGE && in_span < ((int64_t)1 << 31) &&
-                      out_span < ((int64_t)1 << 31);
-    if (GF_SOFF == 2 || fast) {  // 2: the fast form only (the host checks the spans)
-        for (int i0 = zc_begin; i0 < zc_begin + n_steps; i0 += UN) {
-            // the block's base slice zb - 1 may lie outside the array: its slices then never
-            // address memory (their soffset is past the records)
-            const rsrc_t rin = make_rsrc(in_base + ob - sstride, (uint32_t)in_span);
-            const rsrc_t rout = make_rsrc(out_base + os, (uint32_t)out_span);
-            static_for<0, UN>([&](auto kc) { step(kc, std::true_type{}, i0, rin, rout); });
-        }
-    } else if constexpr (GF_SOFF != 2) {
-        for (int i0 = zc_begin; i0 < zc_begin + n_steps; i0 += UN)
-            static_for<0, UN>([&](auto kc) { step(kc, std::false_type{}, i0, rin_null(), rin_null()); });
+                load_p1(BK{}, rs_in(ob + off_a, zb + 2 * R + 1), r_b);
+            if constexpr (GF_PRIO) __builtin_amdgcn_s_setprio(1);
+            if constexpr (!(C::ORDER & 2)) do_p4(tid);
+            lds_barrier();
+            ++zb;
+            ob += sstride;
+            ++zs;
+            os += osstride;
+        });
     }
 }
 
@@ -1378,9 +1243,9 @@ inline bool fused_fast_dtype(int d) { return d == kF32 || d == kU16 || d == kU8 
         auto pick_out = [&](auto tin) -> hipError_t {                                             \
             using TI = decltype(tin);                                                             \
             switch (dout) {                                                                       \
-            case kF32: return launch_fused_pick<R, TY, NT, TI, float>(p, s);                      \
-            case kU16: return launch_fused_pick<R, TY, NT, TI, uint16_t>(p, s);                   \
-            case kU8: case kBool: return launch_fused_pick<R, TY, NT, TI, uint8_t>(p, s);         \
+            case kF32: return launch_fused_auto<R, TY, NT, TI, float>(p, s);                      \
+            case kU16: return launch_fused_auto<R, TY, NT, TI, uint16_t>(p, s);                   \
+            case kU8: case kBool: return launch_fused_auto<R, TY, NT, TI, uint8_t>(p, s);         \
             default: return hipErrorInvalidValue;                                                 \
             }                                                                                     \
         };                                                                                        \

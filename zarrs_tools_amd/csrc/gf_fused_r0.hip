@@ -1,5 +1,5 @@
 // gf_fused_r0.hip — fused guided-filter instantiations for radius 0.
-#include "gf_role.hpp"
+#include "gf_fused.hpp"
 
 namespace zt {
 ZT_FUSED_PAIRS(0, 32, 1024)

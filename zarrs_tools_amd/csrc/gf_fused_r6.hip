@@ -1,5 +1,5 @@
 // gf_fused_r6.hip — fused guided-filter instantiations for radius 6.
-#include "gf_role.hpp"
+#include "gf_fused.hpp"
 
 namespace zt {
 ZT_FUSED_PAIRS(6, 16, 1024)
