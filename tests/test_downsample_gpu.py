@@ -119,14 +119,20 @@ def test_pyramid_levels_bit_exact():
 @pytest.mark.parametrize("shape,dtype", [
     ((37, 50, 71), "uint16"), ((64, 64, 64), "uint8"), ((9, 17, 33), "int16"),
     ((40, 36, 72), "float32"), ((24, 20, 16), "float64"), ((19, 32, 40), "int64"),
-    ((16, 16, 264), "uint32"), ((70, 8, 8), "int8"), ((5, 300, 9), "uint16")])
+    ((16, 16, 264), "uint32"), ((70, 8, 8), "int8"), ((5, 300, 9), "uint16"),
+    # u8 / bool take pyramid3_u8_mean_kernel (16-byte rows, dot4 sums): aligned rows with partial
+    # lanes, rows that are not whole 16-byte quads, odd extents
+    ((33, 34, 35), "uint8"), ((12, 8, 160), "uint8"), ((18, 20, 40), "uint8"),
+    ((16, 12, 1056), "uint8"), ((33, 34, 35), "bool")])
 def test_fused_pyramid_levels_equal_per_level_launches(shape, dtype, monkeypatch):
     """zt_pyramid_downsample fuses up to three 2x2x2 mean levels per launch; every level must be
     bit-identical to the oracle's level-by-level downsample (odd extents, partial workgroups,
     unaligned rows, 8- to 64-bit types) and to the unfused launches."""
     import torch
     rng = np.random.default_rng(sum(shape))
-    if dtype.startswith("float"):
+    if dtype == "bool":
+        v = rng.integers(0, 2, shape).astype(bool)
+    elif dtype.startswith("float"):
         v = (rng.standard_normal(shape) * 1000.0).astype(dtype)
     else:
         info = np.iinfo(dtype)

@@ -208,11 +208,10 @@ __device__ __forceinline__ T pyr_reduce8(const T (&v)[8]) {
     else return pyr_mean8<T>(v);
 }
 
-// XPL level-3 columns per lane: a lane's level-0 rows are 8 XPL elements. 2 for u8 would load
-// 16-byte rows (one KiB per wave-instruction, as u16 rows are), but hipcc then keeps every byte of
-// the 16 rows in a VGPR of its own: 256 VGPRs, one wave per SIMD, and the 2048^3 u8 pyramids took
-// 5.66 ms (mean) / 7.86 ms (mode) against 2.76 ms for the mode at XPL 1 (round 6, tools/bench_ops.py);
-// so 1 everywhere.
+// XPL level-3 columns per lane: a lane's level-0 rows are 8 XPL elements. 2 for u8 through this
+// generic walk would load 16-byte rows, but hipcc then keeps every byte of the 16 rows in a VGPR
+// of its own (256 VGPRs, one wave per SIMD: 5.66 ms mean / 7.86 ms mode at 2048^3 against 2.76 ms
+// for the mode at XPL 1), so u8 takes pyramid3_u8_kernel (packed bytes) and XPL is 1 here.
 template <typename T>
 constexpr int kPyrXpl = 1;
 
@@ -326,9 +325,200 @@ __global__ __launch_bounds__(256) void pyramid3_fused_kernel(const T* __restrict
     }
 }
 
+// The u8 (and bool) pyramids: the same walk with 16-byte level-0 rows per lane (two level-3
+// columns: one KiB per wave-instruction, as the u16 rows), the bytes kept packed. Every window
+// reduction takes two neighbouring windows at once from four 32-bit words: window "lo" is bytes
+// 0 and 1 of each word, window "hi" bytes 2 and 3 (each word one row of the 2x2x2 window, two x),
+// and returns the two results in bytes 0 and 2 of one word.
+//  * mean (downsample.rs:72-97): floor(sum / 8), the exact f64 sum / 8 `as u8` (pyr_mean8); each
+//    pair of bytes summed by v_dot4_u32_u8 against a 0x0101 byte mask (no byte extraction).
+//  * mode (downsample.rs:99-120, ties to the smallest value as pyr_mode8): the 8 values of both
+//    windows as packed 16-bit lanes (v_pk_min_u16 / v_pk_max_u16 sorting network, one issue for
+//    both windows), inverted (255 - v) so that one packed max over the keys run * 256 + (255 - v)
+//    of the sorted runs picks the longest run and, among equal runs, the smallest value.
+//    ~44 VALU per window against ~75 for pyr_mode8 on one window.
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ u16x2 as_u16x2(uint32_t w) { return __builtin_bit_cast(u16x2, w); }
+__device__ __forceinline__ uint32_t as_u32(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+
+template <bool MODE>
+__device__ __forceinline__ uint32_t pyr_u8_pair(const uint32_t (&w)[4]) {
+    if constexpr (!MODE) {
+        uint32_t lo = 0, hi = 0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            lo = __builtin_amdgcn_udot4(w[r], 0x00000101u, lo, false);
+            hi = __builtin_amdgcn_udot4(w[r], 0x01010000u, hi, false);
+        }
+        return (lo >> 3) | ((hi >> 3) << 16);
+    } else {
+        u16x2 s[8];  // inverted values: lane 0 window lo, lane 1 window hi
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const uint32_t iw = ~w[r];
+            s[2 * r] = as_u16x2(__builtin_amdgcn_perm(0u, iw, 0x0c020c00u));      // bytes 0, 2
+            s[2 * r + 1] = as_u16x2(__builtin_amdgcn_perm(0u, iw, 0x0c030c01u));  // bytes 1, 3
+        }
+        auto cx = [&](int i, int j) {
+            const u16x2 lo = __builtin_elementwise_min(s[i], s[j]);
+            const u16x2 hi = __builtin_elementwise_max(s[i], s[j]);
+            s[i] = lo;
+            s[j] = hi;
+        };
+        cx(0, 2); cx(1, 3); cx(4, 6); cx(5, 7);
+        cx(0, 4); cx(1, 5); cx(2, 6); cx(3, 7);
+        cx(0, 1); cx(2, 3); cx(4, 5); cx(6, 7);
+        cx(2, 4); cx(3, 5);
+        cx(1, 4); cx(3, 6);
+        cx(1, 2); cx(3, 4); cx(5, 6);
+        // run = length of the run of equal values ending at i; key = run * 256 + (255 - v)
+        const u16x2 one = {1, 1}, k256 = {256, 256};
+        u16x2 run = one;
+        u16x2 best = s[0] + k256;
+#pragma unroll
+        for (int i = 1; i < 8; ++i) {
+            const u16x2 eq = __builtin_elementwise_sub_sat(one, s[i] - s[i - 1]);  // 1 iff equal
+            run = run * eq + one;
+            best = __builtin_elementwise_max(best, run * k256 + s[i]);
+        }
+        return ~as_u32(best) & 0x00FF00FFu;  // 255 - (255 - v)
+    }
+}
+
+template <int NL, bool VEC, bool MODE>
+__global__ __launch_bounds__(256) void pyramid3_u8_kernel(const uint8_t* __restrict__ in,
+                                                          uint8_t* __restrict__ l1,
+                                                          uint8_t* __restrict__ l2,
+                                                          uint8_t* __restrict__ l3,
+                                                          PyrParams p) {
+    __shared__ uint32_t lds2[4][64];  // a lane's 4 level-2 values, packed
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int dz = w >> 1, dy = w & 1;
+    const int64_t x3 = ((int64_t)blockIdx.x * 64 + lane) * 2;  // first of 2 level-3 columns
+    const int64_t by = blockIdx.y;
+    const int64_t n0y = p.s[0][1], n0x = p.s[0][2];
+    const int64_t n1z = p.s[1][0], n1y = p.s[1][1], n1x = p.s[1][2];
+    const int64_t n2z = p.s[2][0], n2y = p.s[2][1], n2x = p.s[2][2];
+    const int64_t nz1blocks = (n1z + 3) / 4;
+    // bytes 0 and 2 of two pair results -> one word of 4 consecutive outputs
+    auto join = [](uint32_t r0, uint32_t r1) { return __builtin_amdgcn_perm(r1, r0, 0x06040200u); };
+    for (int64_t bz = blockIdx.z; bz < nz1blocks; bz += gridDim.z) {
+        uint32_t v[4][4][4];  // level-0 rows z0b + a, y0b + b: 16 bytes x0b .. x0b + 15
+        const int64_t z0b = 8 * bz + 4 * dz, y0b = 8 * by + 4 * dy, x0b = 8 * x3;
+        const bool xfull = x0b + 16 <= n0x;
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const int64_t z0 = z0b + a, y0 = y0b + b;
+                const bool rok = z0 < p.s[0][0] && y0 < n0y;  // wave-uniform
+                const uint8_t* row = in + (z0 * n0y + y0) * n0x + x0b;
+                if (VEC && rok && xfull) {
+                    const uint4 q = *reinterpret_cast<const uint4*>(row);
+                    v[a][b][0] = q.x; v[a][b][1] = q.y; v[a][b][2] = q.z; v[a][b][3] = q.w;
+                } else {
+#pragma unroll
+                    for (int wd = 0; wd < 4; ++wd) {
+                        uint32_t word = 0;
+#pragma unroll
+                        for (int c = 0; c < 4; ++c) {
+                            const int64_t x = x0b + 4 * wd + c;
+                            word |= (uint32_t)((rok && x < n0x) ? row[4 * wd + c] : 0) << (8 * c);
+                        }
+                        v[a][b][wd] = word;
+                    }
+                }
+            }
+        // level 1: z1 = 4 bz + 2 dz + i, y1 = 4 by + 2 dy + j, x1 = x1b + k (k < 8): word h of
+        // u1[i][j] holds outputs 4h .. 4h + 3; outputs 2q, 2q + 1 come from level-0 word q
+        uint32_t u1[2][2][2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                uint32_t r[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint32_t win[4] = {v[2 * i][2 * j][q], v[2 * i][2 * j + 1][q],
+                                             v[2 * i + 1][2 * j][q], v[2 * i + 1][2 * j + 1][q]};
+                    r[q] = pyr_u8_pair<MODE>(win);
+                }
+                u1[i][j][0] = join(r[0], r[1]);
+                u1[i][j][1] = join(r[2], r[3]);
+            }
+        const int64_t z1b = 4 * bz + 2 * dz, y1b = 4 * by + 2 * dy, x1b = 4 * x3;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int64_t z1 = z1b + i, y1 = y1b + j;
+                if (z1 >= n1z || y1 >= n1y) continue;  // wave-uniform
+                uint8_t* o = l1 + (z1 * n1y + y1) * n1x + x1b;
+                if (VEC && x1b + 8 <= n1x) {
+                    *reinterpret_cast<uint2*>(o) = make_uint2(u1[i][j][0], u1[i][j][1]);
+                } else {
+#pragma unroll
+                    for (int k = 0; k < 8; ++k)
+                        if (x1b + k < n1x) o[k] = (uint8_t)(u1[i][j][k >> 2] >> (8 * (k & 3)));
+                }
+            }
+        // level 2: z2 = 2 bz + dz, y2 = 2 by + dy, x2 = x2b + m (m < 4), packed in one word;
+        // outputs 2h, 2h + 1 come from level-1 word h
+        uint32_t r2[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const uint32_t win[4] = {u1[0][0][h], u1[0][1][h], u1[1][0][h], u1[1][1][h]};
+            r2[h] = pyr_u8_pair<MODE>(win);
+        }
+        const uint32_t u2 = join(r2[0], r2[1]);
+        const int64_t z2 = 2 * bz + dz, y2 = 2 * by + dy, x2 = 2 * x3;
+        if (z2 < n2z && y2 < n2y) {
+            uint8_t* o = l2 + (z2 * n2y + y2) * n2x + x2;
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+                if (x2 + m < n2x) o[m] = (uint8_t)(u2 >> (8 * m));
+        }
+        if constexpr (NL == 3) {
+            lds2[w][lane] = u2;
+            __syncthreads();
+            if (w == 0) {
+                // level 3 x3 + q: level-2 outputs 2q, 2q + 1 of the four waves' words
+                const uint32_t win[4] = {lds2[0][lane], lds2[1][lane], lds2[2][lane], lds2[3][lane]};
+                const uint32_t r3 = pyr_u8_pair<MODE>(win);
+#pragma unroll
+                for (int q = 0; q < 2; ++q)
+                    if (bz < p.s[3][0] && by < p.s[3][1] && x3 + q < p.s[3][2])
+                        l3[(bz * p.s[3][1] + by) * p.s[3][2] + x3 + q] = (uint8_t)(r3 >> (16 * q));
+            }
+            __syncthreads();
+        }
+    }
+}
+
 template <typename T, bool MODE>
 static hipError_t launch_pyr_fused_t(const void* in, void* const* outs, const PyrParams& p,
                                      int nl, hipStream_t s) {
+    if constexpr (std::is_same<T, uint8_t>::value) {
+        const int64_t gx = (p.s[1][2] + 511) / 512, gy = (p.s[1][1] + 3) / 4;
+        const int64_t gz = std::min<int64_t>((p.s[1][0] + 3) / 4, 128);
+        if (gx > 0x7FFFFFFF || gy > 65535) return hipErrorInvalidValue;  // pyramid_fused_grid_fits
+        const bool vec = p.s[0][2] % 16 == 0 && (uintptr_t)in % 16 == 0 &&
+                         (uintptr_t)outs[0] % 8 == 0 && p.s[1][2] % 8 == 0;
+        const dim3 grid((unsigned)gx, (unsigned)gy, (unsigned)gz);
+        const uint8_t* i = static_cast<const uint8_t*>(in);
+        uint8_t* o1 = static_cast<uint8_t*>(outs[0]);
+        uint8_t* o2 = static_cast<uint8_t*>(outs[1]);
+        uint8_t* o3 = nl == 3 ? static_cast<uint8_t*>(outs[2]) : nullptr;
+        if (nl == 3) {
+            if (vec) hipLaunchKernelGGL((pyramid3_u8_kernel<3, true, MODE>), grid, dim3(256), 0, s, i, o1, o2, o3, p);
+            else hipLaunchKernelGGL((pyramid3_u8_kernel<3, false, MODE>), grid, dim3(256), 0, s, i, o1, o2, o3, p);
+        } else {
+            if (vec) hipLaunchKernelGGL((pyramid3_u8_kernel<2, true, MODE>), grid, dim3(256), 0, s, i, o1, o2, o3, p);
+            else hipLaunchKernelGGL((pyramid3_u8_kernel<2, false, MODE>), grid, dim3(256), 0, s, i, o1, o2, o3, p);
+        }
+        return hipGetLastError();
+    }
     constexpr int X = kPyrXpl<T>;
     const int64_t gx = (p.s[1][2] + 256 * X - 1) / (256 * X), gy = (p.s[1][1] + 3) / 4;
     // z capped at 128 workgroup layers, each workgroup looping over level-1 z blocks: 4096^3 u16
