@@ -22,6 +22,9 @@
 #ifndef GF_ORDER_R4
 #define GF_ORDER_R4 2  // r = 4: P4 issued ahead of P12 in C1 (-2 %)
 #endif
+#ifndef GF_ORDER
+#define GF_ORDER 0  // other radii: P4 after P12 in C1
+#endif
 #ifndef GF_PRIO
 #define GF_PRIO 1  // s_setprio phase reordering (measured -4.5% at 2048^3 r=4 with the b128 Hx writes)
 #endif
@@ -517,7 +520,7 @@ struct GFConfig {
     // P12 in C1 (each -2 % at 2048^3, tools/timek.sh); other radii keep the defaults (unmeasured)
     static constexpr bool R4 = R == 4 && TY == 32 && NT == 1024;
     static constexpr int K3 = GF_K3, K4 = R4 ? GF_K4_R4 : GF_K4;
-    static constexpr int ORDER = R4 ? GF_ORDER_R4 : 0;
+    static constexpr int ORDER = R4 ? GF_ORDER_R4 : GF_ORDER;
     static constexpr int K5 = TX * TY / NT;          // outputs per thread (ring width)
     static constexpr int S3 = (E1Y + K3 - 1) / K3;   // segments per column, P3
     static constexpr int S4 = TX / K4;               // segments per row, P4

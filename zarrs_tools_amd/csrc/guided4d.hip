@@ -20,6 +20,7 @@
 #include <cstdlib>
 #include <type_traits>
 
+#include "g4_limits.hpp"
 #include "zt_device.hpp"
 #include "zt_kernels.hpp"
 
@@ -326,9 +327,6 @@ __global__ __launch_bounds__(256) void g4_tab_kernel(double* __restrict__ U3T,
 // later, exactly as g4_tab_kernel forms them from U3. The t-march is unrolled by 2R + 1 so every
 // ring slot is a compile-time register. HBM: v once (+ the apron's L2 / MALL re-reads) and TAB
 // written; the f64 U3 (8 B per input voxel written and read back) never leaves the CU.
-#ifndef G4_TM_MZ
-#define G4_TM_MZ 12  // t-march tile depth (tools/timetshare.hip A/B: 12 beats 8 by 4 %)
-#endif
 #ifndef G4_TM_PFD
 #define G4_TM_PFD 1  // stage loads issued this many steps ahead (1-4 within 2 %)
 #endif
@@ -341,7 +339,7 @@ __global__ __launch_bounds__(256) void g4_tab_kernel(double* __restrict__ U3T,
 #ifndef G4_TM_VP
 #define G4_TM_VP 4  // t-march voxels per thread (along z)
 #endif
-constexpr int kMX = 16, kMY = 16, kMZ = G4_TM_MZ;  // tile (x, y, z)
+constexpr int kMX = 16, kMY = 16, kMZ = kG4TmarchTileZ;  // tile (x, y, z) (g4_limits.hpp)
 constexpr int kMVP = G4_TM_VP, kMNT = kMX * kMY * kMZ / kMVP;  // voxels per thread; threads
 
 // Buffer (SRD) accesses of the t-march: 32-bit byte offsets from a per-step base, out-of-range
@@ -366,17 +364,7 @@ __device__ __forceinline__ int g4_opaque(int v) {
     return v;
 }
 
-// Host check of the t-march's 32-bit offsets. The staged offsets (soff) and the v offsets (voff)
-// are built from the GLOBAL (y, x) of an element, relative to a per-step z-plane base, so they
-// span up to SZ - 1 (= kMZ + 2R - 1) planes of z stride plus a whole plane's (ny - 1) rows of y
-// stride plus nx elements, not one tile's; TAB offsets span kMZ planes of ny * nx pairs. Any span
-// of 2 GiB or more would wrap the (int) offset, and the buffer access would then read 0 silently.
-bool g4_tmarch_offsets_fit(const int64_t* vs3, int ny, int nx, int radius) {
-    const int64_t sz = kMZ + 2 * radius;
-    const int64_t v_span = ((sz - 1) * vs3[1] + (int64_t)(ny - 1) * vs3[2] + nx) * 4;
-    const int64_t t_span = ((int64_t)kMZ * ny * nx) * 8;
-    return v_span < ((int64_t)1 << 31) && t_span < ((int64_t)1 << 31);
-}
+// g4_tmarch_offsets_fit (g4_limits.hpp): the host check of the t-march's 32-bit offsets.
 
 template <int R>
 __global__ __launch_bounds__(kMNT) void g4_tmarch_tab_kernel(const float* __restrict__ v, Str3 vs,
