@@ -123,7 +123,8 @@ def test_pyramid_levels_bit_exact():
     # u8 / bool take pyramid3_u8_mean_kernel (16-byte rows, dot4 sums): aligned rows with partial
     # lanes, rows that are not whole 16-byte quads, odd extents
     ((33, 34, 35), "uint8"), ((12, 8, 160), "uint8"), ((18, 20, 40), "uint8"),
-    ((16, 12, 1056), "uint8"), ((33, 34, 35), "bool")])
+    ((16, 12, 1056), "uint8"), ((33, 34, 35), "bool"), ((12, 8, 160), "int8"),
+    ((33, 34, 35), "int8")])
 def test_fused_pyramid_levels_equal_per_level_launches(shape, dtype, monkeypatch):
     """zt_pyramid_downsample fuses up to three 2x2x2 mean levels per launch; every level must be
     bit-identical to the oracle's level-by-level downsample (odd extents, partial workgroups,
@@ -158,7 +159,10 @@ def test_fused_pyramid_levels_equal_per_level_launches(shape, dtype, monkeypatch
 @pytest.mark.parametrize("shape,dtype,levels", [
     ((37, 50, 71), "uint16", 6), ((64, 64, 64), "uint8", 6), ((9, 17, 33), "int16", 6),
     ((19, 32, 40), "int64", 6), ((16, 16, 264), "uint32", 6), ((70, 8, 8), "int8", 6),
-    ((33, 34, 35), "bool", 6), ((40, 36, 72), "int32", 2)])
+    ((33, 34, 35), "bool", 6), ((40, 36, 72), "int32", 2),
+    # the packed-byte kernel (pyramid3_u8_kernel): 16-byte rows with partial lanes, odd extents
+    ((12, 8, 160), "uint8", 4), ((33, 34, 35), "uint8", 6), ((12, 8, 160), "int8", 4),
+    ((33, 34, 35), "int8", 6), ((16, 16, 96), "bool", 4)])
 def test_fused_mode_pyramid_equals_oracle_levels(shape, dtype, levels):
     """zarrs_ome --discrete on the device: the level-fused mode pyramid (pyr_mode8, up to three
     levels per launch) gives, level by level, the oracle's discrete downsample of the previous

@@ -40,9 +40,10 @@ def bench_pyramid(n, reps, levels, discrete=False, dtype="uint16"):
     from oracle import oracle as O
     ctx = zt.default_context(0)
     x = zt.synth_u16((n, n, n))
-    if dtype == "uint8":  # the low byte of the u16 noise: 256 values, ties and majorities
-        x = (x.view(torch.int16) & 0xFF).to(torch.uint8) if not discrete else \
-            (x.view(torch.int16) & 0x7).to(torch.uint8)
+    if dtype in ("uint8", "int8"):  # the low byte of the u16 noise: 256 values
+        tt = torch.uint8 if dtype == "uint8" else torch.int8
+        x = (x.view(torch.int16) & 0xFF).to(tt) if not discrete else \
+            (x.view(torch.int16) & 0x7).to(tt)
     elif discrete:  # few distinct values, so the mode is not mostly a tie of eight
         x = (x.view(torch.int16) & 0x7).view(torch.uint16)
     esz = x.element_size()
@@ -72,8 +73,8 @@ def bench_pyramid(n, reps, levels, discrete=False, dtype="uint16"):
     sample = O.synth_u16((256, 256, 256))
     if discrete:
         sample = (sample & 0x7).astype(np.dtype(dtype))
-    elif dtype == "uint8":
-        sample = (sample & 0xFF).astype(np.uint8)
+    elif dtype in ("uint8", "int8"):
+        sample = (sample & 0xFF).astype(np.uint8).view(np.dtype(dtype))
     t0 = time.perf_counter()
     O.downsample(sample, dtype, (2, 2, 2), dtype, discrete=discrete)
     cpu_s = time.perf_counter() - t0
@@ -235,6 +236,10 @@ def main():
     if "pyramid_u8" in only:  # the u8 mean pyramid (16-byte rows per lane: 2 level-3 columns)
         print(json.dumps(bench_pyramid(a.pyramid_size, a.reps, a.levels, False, "uint8")),
               flush=True)
+    if "pyramid_i8" in only:  # the i8 mean and mode pyramids (the packed-byte kernel)
+        for disc in (False, True):
+            print(json.dumps(bench_pyramid(a.pyramid_size, a.reps, a.levels, disc, "int8")),
+                  flush=True)
     if "pyramid_discrete" in only:
         for dt in ("uint16", "uint8"):
             print(json.dumps(bench_pyramid(a.pyramid_size, a.reps, a.levels, True, dt)),

@@ -325,26 +325,37 @@ __global__ __launch_bounds__(256) void pyramid3_fused_kernel(const T* __restrict
     }
 }
 
-// The u8 (and bool) pyramids: the same walk with 16-byte level-0 rows per lane (two level-3
+// The u8 / bool / i8 pyramids: the same walk with 16-byte level-0 rows per lane (two level-3
 // columns: one KiB per wave-instruction, as the u16 rows), the bytes kept packed. Every window
 // reduction takes two neighbouring windows at once from four 32-bit words: window "lo" is bytes
 // 0 and 1 of each word, window "hi" bytes 2 and 3 (each word one row of the 2x2x2 window, two x),
 // and returns the two results in bytes 0 and 2 of one word.
-//  * mean (downsample.rs:72-97): floor(sum / 8), the exact f64 sum / 8 `as u8` (pyr_mean8); each
-//    pair of bytes summed by v_dot4_u32_u8 against a 0x0101 byte mask (no byte extraction).
+//  * mean (downsample.rs:72-97): sum / 8 truncated, the exact f64 sum / 8 `as u8` / `as i8`
+//    (pyr_mean8); each pair of bytes summed by v_dot4_u32_u8 (i8: v_dot4_i32_i8) against a
+//    0x0101 byte mask (no byte extraction).
 //  * mode (downsample.rs:99-120, ties to the smallest value as pyr_mode8): the 8 values of both
 //    windows as packed 16-bit lanes (v_pk_min_u16 / v_pk_max_u16 sorting network, one issue for
 //    both windows), inverted (255 - v) so that one packed max over the keys run * 256 + (255 - v)
-//    of the sorted runs picks the longest run and, among equal runs, the smallest value.
+//    of the sorted runs picks the longest run and, among equal runs, the smallest value (i8:
+//    biased by 0x80 first, so the unsigned order is the signed one).
 //    ~44 VALU per window against ~75 for pyr_mode8 on one window.
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ u16x2 as_u16x2(uint32_t w) { return __builtin_bit_cast(u16x2, w); }
 __device__ __forceinline__ uint32_t as_u32(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
 
-template <bool MODE>
+template <bool MODE, bool SGN>
 __device__ __forceinline__ uint32_t pyr_u8_pair(const uint32_t (&w)[4]) {
-    if constexpr (!MODE) {
+    if constexpr (!MODE && SGN) {
+        // i8: v_dot4_i32_i8, then / 8 truncating toward zero (`as i8` of the exact f64 mean)
+        int lo = 0, hi = 0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            lo = __builtin_amdgcn_sdot4((int)w[r], 0x00000101, lo, false);
+            hi = __builtin_amdgcn_sdot4((int)w[r], 0x01010000, hi, false);
+        }
+        return ((uint32_t)(lo / 8) & 0xFFu) | (((uint32_t)(hi / 8) & 0xFFu) << 16);
+    } else if constexpr (!MODE) {
         uint32_t lo = 0, hi = 0;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -353,10 +364,12 @@ __device__ __forceinline__ uint32_t pyr_u8_pair(const uint32_t (&w)[4]) {
         }
         return (lo >> 3) | ((hi >> 3) << 16);
     } else {
+        // i8: the bias v ^ 0x80 maps the signed order onto the unsigned one
+        constexpr uint32_t kBias = SGN ? 0x80808080u : 0u;
         u16x2 s[8];  // inverted values: lane 0 window lo, lane 1 window hi
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const uint32_t iw = ~w[r];
+            const uint32_t iw = ~(w[r] ^ kBias);
             s[2 * r] = as_u16x2(__builtin_amdgcn_perm(0u, iw, 0x0c020c00u));      // bytes 0, 2
             s[2 * r + 1] = as_u16x2(__builtin_amdgcn_perm(0u, iw, 0x0c030c01u));  // bytes 1, 3
         }
@@ -382,11 +395,11 @@ __device__ __forceinline__ uint32_t pyr_u8_pair(const uint32_t (&w)[4]) {
             run = run * eq + one;
             best = __builtin_elementwise_max(best, run * k256 + s[i]);
         }
-        return ~as_u32(best) & 0x00FF00FFu;  // 255 - (255 - v)
+        return (~as_u32(best) & 0x00FF00FFu) ^ (kBias & 0x00FF00FFu);  // 255 - (255 - v), unbiased
     }
 }
 
-template <int NL, bool VEC, bool MODE>
+template <int NL, bool VEC, bool MODE, bool SGN>
 __global__ __launch_bounds__(256) void pyramid3_u8_kernel(const uint8_t* __restrict__ in,
                                                           uint8_t* __restrict__ l1,
                                                           uint8_t* __restrict__ l2,
@@ -442,7 +455,7 @@ __global__ __launch_bounds__(256) void pyramid3_u8_kernel(const uint8_t* __restr
                 for (int q = 0; q < 4; ++q) {
                     const uint32_t win[4] = {v[2 * i][2 * j][q], v[2 * i][2 * j + 1][q],
                                              v[2 * i + 1][2 * j][q], v[2 * i + 1][2 * j + 1][q]};
-                    r[q] = pyr_u8_pair<MODE>(win);
+                    r[q] = pyr_u8_pair<MODE, SGN>(win);
                 }
                 u1[i][j][0] = join(r[0], r[1]);
                 u1[i][j][1] = join(r[2], r[3]);
@@ -469,7 +482,7 @@ __global__ __launch_bounds__(256) void pyramid3_u8_kernel(const uint8_t* __restr
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const uint32_t win[4] = {u1[0][0][h], u1[0][1][h], u1[1][0][h], u1[1][1][h]};
-            r2[h] = pyr_u8_pair<MODE>(win);
+            r2[h] = pyr_u8_pair<MODE, SGN>(win);
         }
         const uint32_t u2 = join(r2[0], r2[1]);
         const int64_t z2 = 2 * bz + dz, y2 = 2 * by + dy, x2 = 2 * x3;
@@ -485,7 +498,7 @@ __global__ __launch_bounds__(256) void pyramid3_u8_kernel(const uint8_t* __restr
             if (w == 0) {
                 // level 3 x3 + q: level-2 outputs 2q, 2q + 1 of the four waves' words
                 const uint32_t win[4] = {lds2[0][lane], lds2[1][lane], lds2[2][lane], lds2[3][lane]};
-                const uint32_t r3 = pyr_u8_pair<MODE>(win);
+                const uint32_t r3 = pyr_u8_pair<MODE, SGN>(win);
 #pragma unroll
                 for (int q = 0; q < 2; ++q)
                     if (bz < p.s[3][0] && by < p.s[3][1] && x3 + q < p.s[3][2])
@@ -499,23 +512,24 @@ __global__ __launch_bounds__(256) void pyramid3_u8_kernel(const uint8_t* __restr
 template <typename T, bool MODE>
 static hipError_t launch_pyr_fused_t(const void* in, void* const* outs, const PyrParams& p,
                                      int nl, hipStream_t s) {
-    if constexpr (std::is_same<T, uint8_t>::value) {
+    if constexpr (sizeof(T) == 1) {  // u8, bool, i8: packed bytes
+        constexpr bool SGN = std::is_signed<T>::value;
         const int64_t gx = (p.s[1][2] + 511) / 512, gy = (p.s[1][1] + 3) / 4;
         const int64_t gz = std::min<int64_t>((p.s[1][0] + 3) / 4, 128);
         if (gx > 0x7FFFFFFF || gy > 65535) return hipErrorInvalidValue;  // pyramid_fused_grid_fits
         const bool vec = p.s[0][2] % 16 == 0 && (uintptr_t)in % 16 == 0 &&
                          (uintptr_t)outs[0] % 8 == 0 && p.s[1][2] % 8 == 0;
         const dim3 grid((unsigned)gx, (unsigned)gy, (unsigned)gz);
-        const uint8_t* i = static_cast<const uint8_t*>(in);
+        const uint8_t* i = static_cast<const uint8_t*>(in);  // i8 as its bytes
         uint8_t* o1 = static_cast<uint8_t*>(outs[0]);
         uint8_t* o2 = static_cast<uint8_t*>(outs[1]);
         uint8_t* o3 = nl == 3 ? static_cast<uint8_t*>(outs[2]) : nullptr;
         if (nl == 3) {
-            if (vec) hipLaunchKernelGGL((pyramid3_u8_kernel<3, true, MODE>), grid, dim3(256), 0, s, i, o1, o2, o3, p);
-            else hipLaunchKernelGGL((pyramid3_u8_kernel<3, false, MODE>), grid, dim3(256), 0, s, i, o1, o2, o3, p);
+            if (vec) hipLaunchKernelGGL((pyramid3_u8_kernel<3, true, MODE, SGN>), grid, dim3(256), 0, s, i, o1, o2, o3, p);
+            else hipLaunchKernelGGL((pyramid3_u8_kernel<3, false, MODE, SGN>), grid, dim3(256), 0, s, i, o1, o2, o3, p);
         } else {
-            if (vec) hipLaunchKernelGGL((pyramid3_u8_kernel<2, true, MODE>), grid, dim3(256), 0, s, i, o1, o2, o3, p);
-            else hipLaunchKernelGGL((pyramid3_u8_kernel<2, false, MODE>), grid, dim3(256), 0, s, i, o1, o2, o3, p);
+            if (vec) hipLaunchKernelGGL((pyramid3_u8_kernel<2, true, MODE, SGN>), grid, dim3(256), 0, s, i, o1, o2, o3, p);
+            else hipLaunchKernelGGL((pyramid3_u8_kernel<2, false, MODE, SGN>), grid, dim3(256), 0, s, i, o1, o2, o3, p);
         }
         return hipGetLastError();
     }
