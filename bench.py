@@ -220,6 +220,23 @@ def load_traffic(gshape, radius: int, world: int, share=None):
     only when it was measured on this exact library build and workload — the same global shape,
     radius and world size, and for a `--share G/N` proxy the same (G, N) share (entries without a
     "share" key describe the whole volume); else None."""
+    e = load_traffic_entry(gshape, radius, world, share)
+    return e.get("hbm_bytes_per_launch") if e else None
+
+
+def load_sq(gshape, radius: int, world: int, share=None):
+    """The SQ instruction counters per voxel (VALU, SALU, LDS, VMEM) and wave-cycle ratios of the
+    same keyed PMC entry, or None."""
+    e = load_traffic_entry(gshape, radius, world, share)
+    if not e or "sq_per_voxel" not in e:
+        return None
+    return {"insts_per_voxel": e["sq_per_voxel"],
+            "wave_cycle_ratios": e.get("sq_wave_cycle_ratios"),
+            "source": "rocprofv3 --pmc SQ_* passes of the same build (tools/profile_pmc.sh)"}
+
+
+def load_traffic_entry(gshape, radius: int, world: int, share=None):
+    """The profiles/pmc_traffic.json entry of this build and workload (see load_traffic)."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     want_share = list(share) if share is not None else None
     try:
@@ -230,7 +247,7 @@ def load_traffic(gshape, radius: int, world: int, share=None):
             if (e.get("lib_sha256") == lib_hash() and list(e.get("global_shape", [])) == list(gshape)
                     and e.get("radius") == radius and e.get("world", 1) == world
                     and e.get("share") == want_share):
-                return e.get("hbm_bytes_per_launch")
+                return e
     except (OSError, ValueError, AttributeError):
         pass
     return None
@@ -297,7 +314,8 @@ def leg_g2(ctx, L, stream, warmup, reps):
     return {"config": "BASELINE configs[1]: guided_filter r=2 on 1024^3 f32, 256^3 chunks, "
                       "1 GPU device-resident", "ms": round(ms, 4),
             "value": round(vox * 4 / 2 ** 30 / (ms / 1e3), 3), "unit": "GiB/s",
-            "roofline": _roof(vox * ALGO_BYTES_PER_VOXEL, ms, load_traffic(gshape, radius, 1)),
+            "roofline": dict(_roof(vox * ALGO_BYTES_PER_VOXEL, ms, load_traffic(gshape, radius, 1)),
+                             sq=load_sq(gshape, radius, 1)),
             "parity": {k: par[k] for k in ("max_rel", "tol", "ok", "chunks", "bit_exact_frac")}}
 
 
@@ -738,6 +756,7 @@ def main():
         # access pattern runs to the memory system's rate, next to the algorithmic `achieved`
         res["roofline"]["traffic_gbs"] = round(traffic / (kern_ms / 1000.0) / 1e9, 1)
         res["roofline"]["traffic_frac"] = round(res["roofline"]["traffic_gbs"] / HBM_PEAK_GBS, 4)
+    res["roofline"]["sq"] = load_sq(gshape, radius, world, share)
     if share is not None:
         res["metric"] += f", rank {share[0]}'s share of a {share[1]}-GPU split (1-GPU proxy)"
         res["config"]["parallelism"] = f"share {share[0]}/{share[1]} on one GPU"

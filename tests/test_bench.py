@@ -78,3 +78,26 @@ def test_traffic_entries_are_keyed_to_build_workload_and_world(monkeypatch, tmp_
     # the single-entry form of earlier rounds still reads
     (tmp_path / "profiles" / "pmc_traffic.json").write_text(json.dumps(entries[0]))
     assert bench.load_traffic((2048,) * 3, 4, 1) == 1.0e11
+
+
+def test_sq_counters_follow_the_traffic_key(monkeypatch, tmp_path):
+    """The SQ instruction counters per voxel (report G2's SALU / voxel in its leg)
+    ride on the same keyed PMC entry as the traffic: reported only for this build and workload."""
+    import json
+    (tmp_path / "profiles").mkdir()
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    monkeypatch.setattr(bench, "lib_hash", lambda: "abc")
+    sq = {"VALU": 0.85, "SALU": 0.42, "LDS": 0.18}
+    entries = [{"lib_sha256": "abc", "global_shape": [1024] * 3, "radius": 2, "world": 1,
+                "hbm_bytes_per_launch": 2.0e10, "sq_per_voxel": sq,
+                "sq_wave_cycle_ratios": {"WAIT_INST_ANY": 0.36}},
+               {"lib_sha256": "abc", "global_shape": [2048] * 3, "radius": 4, "world": 1,
+                "hbm_bytes_per_launch": 1.0e11},
+               {"lib_sha256": "old", "global_shape": [512] * 3, "radius": 2, "world": 1,
+                "hbm_bytes_per_launch": 3.0e9, "sq_per_voxel": sq}]
+    (tmp_path / "profiles" / "pmc_traffic.json").write_text(json.dumps({"entries": entries}))
+    got = bench.load_sq((1024,) * 3, 2, 1)
+    assert got["insts_per_voxel"] == sq and got["wave_cycle_ratios"] == {"WAIT_INST_ANY": 0.36}
+    assert bench.load_sq((2048,) * 3, 4, 1) is None  # traffic only, no SQ passes
+    assert bench.load_sq((512,) * 3, 2, 1) is None  # another build
+    assert bench.load_traffic((1024,) * 3, 2, 1) == 2.0e10

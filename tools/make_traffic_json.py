@@ -112,6 +112,24 @@ def main():
                    "bytes; Infinity-Cache hits are counted by these counters"}
     if share is not None:
         d["share"] = share
+    # the SQ instruction counters of the same kernel (tools/profile_pmc.sh passes sq1 / sq2),
+    # per output voxel, and the wave-cycle ratios: reported beside the traffic by bench.py
+    sq = {}
+    for pas in ("sq1", "sq2"):
+        for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD",
+                  "SQ_INSTS_VMEM_WR", "SQ_WAVE_CYCLES", "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY",
+                  "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_LDS"):
+            v, n = total(os.path.join(pmc, pas), c)
+            if n:
+                sq[c] = v / n  # per launch
+    if sq:
+        d["sq_per_voxel"] = {k[len("SQ_INSTS_"):]: round(sq[k] / vox, 4) for k in sq
+                             if k.startswith("SQ_INSTS_")}
+        wc = sq.get("SQ_WAVE_CYCLES")
+        if wc:
+            d["sq_wave_cycle_ratios"] = {k[len("SQ_"):] : round(sq[k] / wc, 4) for k in
+                                         ("SQ_WAIT_INST_ANY", "SQ_WAIT_ANY",
+                                          "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_LDS") if k in sq}
     # merge: one entry per (shape, radius, world); entries of other builds are dropped
     entries = []
     if os.path.exists(out):
