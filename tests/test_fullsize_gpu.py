@@ -8,7 +8,8 @@ compared bit-exactly with the oracle's downsample of the same input region (down
 
   G2  guided_filter r=2, 1024^3 f32, 256^3 chunks        (BASELINE configs[1])
   G3  guided_filter r=4, 2048^3 f32, 256^3 chunks        (configs[2], the metric)
-  P   5-level 2x mean pyramid of a 2048^3 u16 per-GPU octant of configs[3]'s 4096^3
+  P   5-level 2x mean pyramid of a 2048^3 u16 per-GPU octant of configs[3]'s 4096^3; the same
+      size in u8 / i8, mean and mode (the packed-byte kernel)
   T   one GPU's share of configs[4]: rank 5's (t, z) block of the (2, 4) split of (32, 1024^3)
       f32 (output t [16, 32) x z [256, 512) from its 20 x 264-plane halo'd input block,
       shard.block_assignment), chunks (4, 256^3), r=2
@@ -116,6 +117,36 @@ def test_p_pyramid_2048_u16_levels_bit_exact():
         if prev.shape[0] > 256:
             prev = prev[:256, :256, :256]
         want = O.downsample(prev.cpu().numpy(), "uint16", (2, 2, 2), "uint16")
+        got = levels[k][:want.shape[0], :want.shape[1], :want.shape[2]].cpu().numpy()
+        np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.parametrize("dtype,discrete", [("uint8", False), ("uint8", True),
+                                             ("int8", False), ("int8", True)])
+def test_pyramid_2048_bytes_levels_bit_exact(dtype, discrete):
+    """The packed-byte pyramid kernel (pyramid3_u8_kernel: 16-byte rows, dot4 means, packed 16-bit
+    sorting-network mode) at config P's per-GPU size: 5 levels of a 2048^3 u8 / i8 volume (the
+    low byte of the synthetic u16; for the mode its low 3 bits, so majorities and ties occur)."""
+    import torch
+    shape = (2048,) * 3
+    mask = 0x7 if discrete else 0xFF
+    tt = torch.uint8 if dtype == "uint8" else torch.int8
+    x = (zt.synth_u16(shape).view(torch.int16) & mask).to(tt)
+    torch.cuda.synchronize()
+    levels = zt.pyramid(x, (2, 2, 2), max_levels=5, discrete=discrete)
+    torch.cuda.synchronize()
+    del x
+    for o in [(0, 0, 0), (448, 320, 576), (896, 896, 896)]:
+        src = O.synth_block_nd([2 * c for c in o], (256,) * 3, shape, "uint16")
+        src = (src & mask).astype(np.uint8).view(np.dtype(dtype))
+        want = O.downsample(src, dtype, (2, 2, 2), dtype, discrete=discrete)
+        got = levels[0][o[0]:o[0] + 128, o[1]:o[1] + 128, o[2]:o[2] + 128].cpu().numpy()
+        np.testing.assert_array_equal(got, want)
+    for k in range(1, 5):
+        prev = levels[k - 1]
+        if prev.shape[0] > 256:
+            prev = prev[:256, :256, :256]
+        want = O.downsample(prev.cpu().numpy(), dtype, (2, 2, 2), dtype, discrete=discrete)
         got = levels[k][:want.shape[0], :want.shape[1], :want.shape[2]].cpu().numpy()
         np.testing.assert_array_equal(got, want)
 
