@@ -52,12 +52,6 @@
 #ifndef GF_P1PFD_R2
 #define GF_P1PFD_R2 2  // the same at r <= 2 (stage-1 ring: entering quads only)
 #endif
-#ifndef GF_QPL_R4
-#define GF_QPL_R4 1  // r = 4: stage-1 quads per P12 lane (2: 8 consecutive x per lane)
-#endif
-#ifndef GF_P1PFD_Q2
-#define GF_P1PFD_Q2 1  // prefetch depth with 2 quads per lane
-#endif
 #ifndef GF_WAVE_SKIP
 #define GF_WAVE_SKIP 1  // P4: idle waves branch around the phase
 #endif
@@ -533,7 +527,7 @@ struct GFConfig {
     static constexpr int N3 = E1X * S3, N4 = E1Y * S4;  // work items
     // P12: one lane per quad (4 consecutive x) of an E2 row, whole rows per wave, so the
     // x-neighbour quads of the window sums come from adjacent lanes (DPP), never across waves
-    static constexpr int QPL = R4 ? GF_QPL_R4 : 1;  // quads per lane
+    static constexpr int QPL = 1;  // quads per lane
     static constexpr int EPL = 4 * QPL;                    // elements per lane
     static constexpr int NQ1X = E2X / EPL;                 // lanes per E2 row
     static constexpr int RPW = 64 / NQ1X;                  // E2 rows per wave
@@ -666,8 +660,7 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     // ---- per-thread, step-invariant quad offsets and in-domain masks -----------------------
     const int tid0 = threadIdx.x;
     constexpr int EPL = C::EPL;
-    constexpr int QPL = C::QPL;
-    int q1off[C::NQP1][QPL], q1mask[C::NQP1][QPL];
+    int q1off[C::NQP1], q1mask[C::NQP1];
     // P12 lane -> (E2 row, lane item = 4 consecutive x) for pass k
     auto p12_pos = [&](int tid, int k, int& row, int& cq) -> bool {
         const int w = tid / 64 - C::W12, l = tid % 64;
@@ -679,31 +672,18 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     for (int k = 0; k < C::NQP1; ++k) {
         int row, cq;
         const bool valid = p12_pos(tid0, k, row, cq);
+        const int gx = x0 - 2 * R + EPL * cq, gy = y0 - 2 * R + row;
+        int m = 0;
+        if (valid && gy >= 0 && gy < ny) {
 #pragma unroll
-        for (int qd = 0; qd < QPL; ++qd) {
-            const int gx = x0 - 2 * R + EPL * cq + 4 * qd, gy = y0 - 2 * R + row;
-            int m = 0;
-            if (valid && gy >= 0 && gy < ny) {
-#pragma unroll
-                for (int e = 0; e < 4; ++e) m |= (gx + e >= 0 && gx + e < nx) ? (1 << e) : 0;
-            }
-            q1mask[k][qd] = m;
-            q1off[k][qd] = (EDGE ? valid : m == 0xF) ? (gy * sy + gx) * ESZ : kBadOff;
+            for (int e = 0; e < 4; ++e) m |= (gx + e >= 0 && gx + e < nx) ? (1 << e) : 0;
         }
+        q1mask[k] = m;
+        q1off[k] = (EDGE ? valid : m == 0xF) ? (gy * sy + gx) * ESZ : kBadOff;
     }
     auto load_quad = [&](rsrc_t r, int off, int mask, SI (&v)[4]) {
         if constexpr (EDGE) load_quad_masked<TIn>(r, off, mask, v);
         else Quad<TIn>::load(r, off, v);
-    };
-    // the EPL elements of a lane's item in pass k: QPL quads
-    auto load_item = [&](rsrc_t r, int k, SI (&v)[EPL]) {
-#pragma unroll
-        for (int qd = 0; qd < QPL; ++qd) {
-            SI q[4];
-            load_quad(r, q1off[k][qd], q1mask[k][qd], q);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[4 * qd + e] = q[e];
-        }
     };
 
     SA zv[C::NQP1][EPL];
@@ -725,10 +705,10 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
             const rsrc_t rs = slice_rsrc(zc_begin - 1 - R + j);  // 0 outside [zlo, zhi)
 #pragma unroll
             for (int k = 0; k < C::NQP1; ++k) {
-                SI v[EPL];
-                load_item(rs, k, v);
+                SI v[4];
+                load_quad(rs, q1off[k], q1mask[k], v);
 #pragma unroll
-                for (int e = 0; e < EPL; ++e) {
+                for (int e = 0; e < 4; ++e) {
                     ring1[(j + W - 1) % W][k][e] = v[e];
                     zv[k][e] += (SA)v[e];
                 }
@@ -740,10 +720,10 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
             const rsrc_t rs = slice_rsrc(z);
 #pragma unroll
             for (int k = 0; k < C::NQP1; ++k) {
-                SI v[EPL];
-                load_item(rs, k, v);
+                SI v[4];
+                load_quad(rs, q1off[k], q1mask[k], v);
 #pragma unroll
-                for (int e = 0; e < EPL; ++e) zv[k][e] += (SA)v[e];
+                for (int e = 0; e < 4; ++e) zv[k][e] += (SA)v[e];
             }
         }
     }
@@ -763,8 +743,7 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
     // box where the march took 30 ms, neutral on a 28.7 ms box, u16 -1 to -3 %; r = 1, 2 -1 to
     // -3.6 %); one step elsewhere (r = 3 / 5 measured +0.5-0.9 %; r > 5 and the masked edge mode
     // spill the second buffer).
-    constexpr int PF = EDGE ? 1 : (R == 4 && QPL == 2) ? GF_P1PFD_Q2 : R == 4 ? GF_P1PFD
-                                : R <= 2 ? GF_P1PFD_R2 : 1;
+    constexpr int PF = EDGE ? 1 : R == 4 ? GF_P1PFD : R <= 2 ? GF_P1PFD_R2 : 1;
     SI pa[PF][C::NQP1][EPL], ps[PF][C::NQP1][EPL];
     float vc[C::K3];  // v of the next P3 slice at this thread's item (prefetched)
     float v5[K5];     // v of the next P5 output slice at this thread's outputs
@@ -774,11 +753,11 @@ __global__ __launch_bounds__(NT) void gf3d_fused_kernel(GFParams p) {
         constexpr int b = decltype(bc)::value;
 #pragma unroll
         for (int k = 0; k < C::NQP1; ++k) {
-            SI a4[EPL], s4[EPL];
-            load_item(ra, k, a4);
-            if constexpr (!C::P1RING) load_item(rs, k, s4);
+            SI a4[4], s4[4];
+            load_quad(ra, q1off[k], q1mask[k], a4);
+            if constexpr (!C::P1RING) load_quad(rs, q1off[k], q1mask[k], s4);
 #pragma unroll
-            for (int e = 0; e < EPL; ++e) {
+            for (int e = 0; e < 4; ++e) {
                 pa[b][k][e] = a4[e];
                 if constexpr (!C::P1RING) ps[b][k][e] = s4[e];
             }
