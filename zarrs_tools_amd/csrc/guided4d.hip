@@ -586,7 +586,9 @@ __device__ __forceinline__ void store_dtype(void* out, int dtype, int64_t i, flo
 // one output timepoint; the running z-window (f64 pair) covers the tile's R apron, whose loads
 // reach into the block's halo (zero outside the block: the clamped windows). The leaving slice
 // comes from a register ring when it fits (box3_ring), as in box3_march_kernel.
-// TYF: output tile height (kTY; 64 x 32 tiles measured 55.9 against 54.0 ms on the T share)
+// TYF: output tile height (kTY; 64 x 32 tiles measured 55.9 against 54.0 ms on the T share in
+// round 4, and in the F32 form 14.64 against 13.76 ms per launch in round 6:
+// profiles/r06_box3final_ty32.txt)
 // F32 (f32 output, unit x strides, 32-bit offsets checked on the host: box3_final_f32_fits):
 // every global access is a buffer access with an out-of-range offset instead of a branch, the
 // step barriers wait for LDS only and the march runs whole blocks of 2R + 1 steps (the padded
