@@ -411,6 +411,9 @@ __global__ __launch_bounds__(kMNT) void g4_tmarch_tab_kernel(const float* __rest
         const bool in = e < NS && gz >= 0 && gz < nz && gy >= 0 && gy < ny && gx >= 0 && gx < nx;
         soff[k] = in ? (int)(((ez + zsh) * vs.z + gy * vs.y + gx) * 4) : kG4Bad;
     }
+    // (soff, voff and toff are step-invariant registers with kG4Bad already selected, so the
+    //  accesses take them as they are: passing them through g4_opaque added a register copy per
+    //  access, 1 % of the T share, profiles/r06_plain_offsets.txt)
     // staged values of steps t + 1 .. t + PFD (pre[0 .. PFD - 1]): the loads of a step stay in
     // flight for PFD steps
     constexpr int PFD = G4_TM_PFD;
@@ -419,7 +422,7 @@ __global__ __launch_bounds__(kMNT) void g4_tmarch_tab_kernel(const float* __rest
         const bool ok = (unsigned)t < (unsigned)T;
         const g4rsrc r = g4_rsrc(v + (ok ? (int64_t)t * vs.t + vbase : 0), ok ? 0x7FFFFFF0u : 0u);
 #pragma unroll
-        for (int k = 0; k < NPS; ++k) dst[k] = g4_ld(r, g4_opaque(soff[k]));
+        for (int k = 0; k < NPS; ++k) dst[k] = g4_ld(r, soff[k]);
     };
 
     // this thread's voxels: (x, y) and VP consecutive z
@@ -468,7 +471,7 @@ __global__ __launch_bounds__(kMNT) void g4_tmarch_tab_kernel(const float* __rest
                 const g4rsrc r = g4_rsrc(v + (ok ? (int64_t)tau * vs.t + (int64_t)z0 * vs.z : 0),
                                          ok ? 0x7FFFFFF0u : 0u);
 #pragma unroll
-                for (int q = 0; q < VP; ++q) vt[q] = g4_ld(r, g4_opaque(voff[q]));
+                for (int q = 0; q < VP; ++q) vt[q] = g4_ld(r, voff[q]);
             }
             double u3[VP];
 #pragma unroll
@@ -559,7 +562,7 @@ __global__ __launch_bounds__(kMNT) void g4_tmarch_tab_kernel(const float* __rest
                 rab[sab][q] = ab;
                 const float2 o = make_float2((float)SA[q], (float)SB[q]);
                 __builtin_amdgcn_raw_buffer_store_b64(
-                    (u32x2g4){__float_as_uint(o.x), __float_as_uint(o.y)}, rt, g4_opaque(toff[q]), 0, 0);
+                    (u32x2g4){__float_as_uint(o.x), __float_as_uint(o.y)}, rt, toff[q], 0, 0);
             }
         });
     }
