@@ -644,12 +644,29 @@ __global__ __launch_bounds__(RING ? kTX * TYF / 2 : kNT) void box3_final_kernel(
         pidx[k] = (e < NE && gy >= 0 && gy < ny && gx >= 0 && gx < nx) ? (PI)gy * nx + gx : (PI)-1;
     }
     float2* const Zf = &Z[0][0];
+    // F32: the byte offsets of the owned apron points, this thread's v loads and output stores,
+    // selected once (kG4Bad outside) and used as they are at every access
+    int boff[NPT], vof[KY], oof[KY];
+    if constexpr (F32) {
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) boff[k] = pidx[k] >= 0 ? (int)pidx[k] * 8 : kG4Bad;
+        const int tx = threadIdx.x % kTX, sy = (threadIdx.x / kTX) * KY;
+        const int gx = x0 + tx;
+#pragma unroll
+        for (int j = 0; j < KY; ++j) {
+            const int gy = y0 + sy + j;
+            const bool in = gx < ox1 && gy < oy1;
+            vof[j] = in ? (int)((gy * vs.y + gx) * 4) : kG4Bad;
+            oof[j] = in ? (int)(((gy - oy0) * g.out_strides[2] + (gx - ox0)) * 4) : kG4Bad;
+        }
+    }
+    // (selected at the access instead, through g4_opaque: box3_final 14.20 against 14.08 ms,
+    //  profiles/r06_plain_offsets.txt)
     auto load = [&](int z, int k) -> float2 {
         if constexpr (F32) {
             const bool ok = (unsigned)z < (unsigned)nz;
             const g4rsrc r = g4_rsrc(vol + (ok ? (int64_t)z * plane : 0), ok ? 0x7FFFFFF0u : 0u);
-            const u32x2g4 q = __builtin_amdgcn_raw_buffer_load_b64(
-                r, g4_opaque(pidx[k] >= 0 ? (int)pidx[k] * 8 : kG4Bad), 0, 0);
+            const u32x2g4 q = __builtin_amdgcn_raw_buffer_load_b64(r, boff[k], 0, 0);
             return make_float2(__uint_as_float(q.x), __uint_as_float(q.y));
         } else {
             return (pidx[k] >= 0 && z >= 0 && z < nz) ? vol[(int64_t)z * plane + pidx[k]]
@@ -664,17 +681,11 @@ __global__ __launch_bounds__(RING ? kTX * TYF / 2 : kNT) void box3_final_kernel(
     // waiting for it does not wait for the prefetch (vmcnt counts in issue order)
     auto v_load = [&](int z, float (&vv)[KY]) {
         if constexpr (F32) {
-            const int tx = threadIdx.x % kTX, sy = (threadIdx.x / kTX) * KY;
-            const int gx = x0 + tx;
             const bool zok = z < z1;
             const g4rsrc rv = g4_rsrc(v + (zok ? t * vs.t + (int64_t)z * vs.z : 0),
                                       zok ? 0x7FFFFFF0u : 0u);
 #pragma unroll
-            for (int j = 0; j < KY; ++j) {
-                const int gy = y0 + sy + j;
-                const bool in = gx < ox1 && gy < oy1;
-                vv[j] = g4_ld(rv, g4_opaque(in ? (int)((gy * vs.y + gx) * 4) : kG4Bad));
-            }
+            for (int j = 0; j < KY; ++j) vv[j] = g4_ld(rv, vof[j]);
         }
     };
     // x / y windows of the Z slice of output slice z and the final stage
@@ -718,10 +729,8 @@ __global__ __launch_bounds__(RING ? kTX * TYF / 2 : kNT) void box3_final_kernel(
                     static_cast<float*>(out) +
                         (zok ? ot * g.out_strides[0] + (int64_t)(z - oz0) * g.out_strides[1] : 0),
                     zok ? 0x7FFFFFF0u : 0u);
-                __builtin_amdgcn_raw_buffer_store_b32(
-                    __float_as_uint(o), ro,
-                    g4_opaque(in ? (int)(((gy - oy0) * g.out_strides[2] + (gx - ox0)) * 4) : kG4Bad),
-                    0, 2);
+                (void)in;
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(o), ro, oof[j], 0, 2);
             } else if (gx < ox1 && gy < oy1) {
                 const float cnt = (float)(czx * ccount(gy, ny, R));
                 const float ma = (float)sacc.x / cnt, mb = (float)sacc.y / cnt;
