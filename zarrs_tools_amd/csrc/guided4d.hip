@@ -366,6 +366,24 @@ __device__ __forceinline__ int g4_opaque(int v) {
 
 // g4_tmarch_offsets_fit (g4_limits.hpp): the host check of the t-march's 32-bit offsets.
 
+// x / d for an integer count d given rcp = RN(1/d): Markstein's correction makes the quotient
+// correctly rounded (= IEEE division) in 3 VALU ops (as gf_fused.hpp's div_by_count).
+__device__ __forceinline__ float g4_div_by_count(float x, float d, float rcp) {
+    const float q = x * rcp;
+    const float r = __builtin_fmaf(-q, d, x);
+    return __builtin_fmaf(r, rcp, q);
+}
+// s / (s + eps): rcp, one Newton step and Markstein's correction (within 1 ulp, almost always
+// correctly rounded; 0/0 gives NaN as in the reference), as gf_fused.hpp's fast_div.
+__device__ __forceinline__ float g4_fast_div(float x, float d) {
+    float y = __builtin_amdgcn_rcpf(d);
+    const float e = __builtin_fmaf(-d, y, 1.0f);
+    y = __builtin_fmaf(e, y, y);
+    const float q = x * y;
+    const float r = __builtin_fmaf(-d, q, x);
+    return __builtin_fmaf(r, y, q);
+}
+
 template <int R>
 __global__ __launch_bounds__(kMNT) void g4_tmarch_tab_kernel(const float* __restrict__ v, Str3 vs,
                                                              float2* __restrict__ TAB, int T,
@@ -385,6 +403,11 @@ __global__ __launch_bounds__(kMNT) void g4_tmarch_tab_kernel(const float* __rest
     __shared__ float Vs[SZ][SY][SX];
     __shared__ double Xs[SZ][SY][kMX];
     __shared__ double Ys[SZ][kMY][kMX];
+    // RN(1/c) for the 4-D window counts c <= (2R+1)^4 (u by Markstein's correction: = IEEE)
+    constexpr int W4 = (2 * R + 1) * (2 * R + 1) * (2 * R + 1) * (2 * R + 1);
+    __shared__ float rtab[W4 + 1];
+    for (int c = threadIdx.x; c <= W4; c += kMNT) rtab[c] = c > 0 ? 1.0f / (float)c : 0.0f;
+    g4_lds_barrier();
 
     // XCD-aware block order (xcd_block): each XCD marches a contiguous run of neighbouring tiles
     const int64_t nb = gridDim.x;
@@ -447,6 +470,7 @@ __global__ __launch_bounds__(kMNT) void g4_tmarch_tab_kernel(const float* __rest
     double ru[W][VP];   // U3 ring: slot (t - tb) % W holds U3(t)
     float2 rab[W][VP];  // (a, b) ring: slot (tau - tb) % W holds ab(tau)
     double SA[VP], SB[VP];  // running t-window sums of (a, b) (exact: f64 sums of f32 values)
+
 #pragma unroll
     for (int q = 0; q < VP; ++q) {
         SA[q] = SB[q] = 0.0;
@@ -546,14 +570,16 @@ __global__ __launch_bounds__(kMNT) void g4_tmarch_tab_kernel(const float* __rest
 #pragma unroll
             for (int q = 0; q < VP; ++q) {
                 ru[su][q] = u3[q];
-                double U4 = 0.0;  // the ring's sum (exact: any order)
+                double U4 = 0.0;  // the ring's sum (exact: any order; a running sum spills)
 #pragma unroll
                 for (int j = 0; j < W; ++j) U4 += ru[j][q];
-                const float cnt = (float)(c3[q] * ct);
-                const float u = (float)U4 / cnt;  // summed_area_table_mean (IEEE division)
+                // u = RN(U4) / c (summed_area_table_mean: Markstein = IEEE division); a within
+                // 1 ulp (IEEE divisions here: 1.2 % slower, profiles/r06_tmarch_fastdiv.txt)
+                const int ci = c3[q] * ct;
+                const float u = g4_div_by_count((float)U4, (float)ci, rtab[ci]);
                 const float d = vt[q] - u;
                 const float sq = d * d;  // (v - u).powf(2.0)
-                const float a = sq / (sq + eps);
+                const float a = g4_fast_div(sq, sq + eps);
                 const float2 ab = need_ab ? make_float2(a, (1.0f - a) * u) : make_float2(0.f, 0.f);
                 SA[q] += (double)ab.x;
                 SB[q] += (double)ab.y;
