@@ -13,7 +13,8 @@
 //   K3f box3_final_kernel: the box3 z-march of TAB over the output box with the final stage,
 //       mean = RN_f32(S4) / c4, out = RN(RN(v * mean_a) + mean_b) cast to TOut
 //       (guided_filter.rs:144-163, :101-102).
-// Every division is IEEE (correctly rounded), stage 1 exact, stage 2 with f64 t-sums.
+// Divisions: u = RN(U) / c correctly rounded (IEEE, or Markstein with RN(1/c) in the t-march), a
+// within 1 ulp in the t-march (IEEE elsewhere); stage 1 exact, stage 2 with f64 t-sums.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
