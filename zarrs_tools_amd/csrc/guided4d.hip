@@ -319,10 +319,10 @@ __global__ __launch_bounds__(256) void g4_tab_kernel(double* __restrict__ U3T,
 }
 
 // ---- t-march stage 1 (round 5): K1 and K2t in one kernel, no U3 in HBM --------------------------
-// One workgroup owns a 16 x 16 x 8 (x, y, z) tile of the TAB region (the output box + R, clamped to
+// One workgroup owns a 16 x 16 x kMZ (x, y, z) tile of the TAB region (the output box + R, clamped to
 // the block) and marches along t. Per step t it stages v(t) on the tile + 2R apron in LDS and forms
 // U3(t) = the exact f64 3-D window sums of its voxels (x, y passes through LDS, the z pass from LDS
-// into registers); each thread keeps, for its 2 voxels, a register ring of the last 2R + 1 U3 and
+// into registers); each thread keeps, for its VP voxels, a register ring of the last 2R + 1 U3 and
 // (a, b) values, so U4 = the t-window of U3 (exact), u, a, b (guided_filter.rs:126-142 with 4-D
 // counts) and TAB = the t-window sums of (a, b) (f64, rounded to f32 once) follow R and 2R steps
 // later, exactly as g4_tab_kernel forms them from U3. The t-march is unrolled by 2R + 1 so every
@@ -338,7 +338,8 @@ __global__ __launch_bounds__(256) void g4_tab_kernel(double* __restrict__ U3T,
 #define G4_TM_KY 4  // t-march y-pass outputs per item
 #endif
 #ifndef G4_TM_VP
-#define G4_TM_VP 4  // t-march voxels per thread (along z)
+#define G4_TM_VP 3  // t-march voxels per thread (along z): 1024 threads, 128 VGPRs, 4 waves per SIMD
+                    // (4 voxels: 768 threads, 3 waves, 1.6 % slower; profiles/r06_tmarch_vp3.txt)
 #endif
 constexpr int kMX = 16, kMY = 16, kMZ = kG4TmarchTileZ;  // tile (x, y, z) (g4_limits.hpp)
 constexpr int kMVP = G4_TM_VP, kMNT = kMX * kMY * kMZ / kMVP;  // voxels per thread; threads
